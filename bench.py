@@ -1,0 +1,223 @@
+"""Headline benchmark: decoded key bits/s of the N=10240 R=0.49 code at QBER 0.02,
+<= 50 sum-product iterations, message clamp 100 (BASELINE.json configs[1]).
+
+One step = one QBER-point batch of F=4096 frames through the hot path, keys
+already resident in HBM: LLR init, Alice's syndrome, flooding sum-product
+decode, key comparison and the batch counters (qkd_qkd_ldpc_batch +
+qkd_counters_batch). Key pairs are generated once on the device beforehand
+with the reference's seeding (SIMULATION_SEED=777, frame k -> seeds[k]).
+
+Multi-GPU (torchrun, one process per GPU): frames shard with no data-path
+collective; rank r decodes frames [r*F, (r+1)*F) of the seed stream (weak
+scaling) and the counters are summed with one all-reduce per step.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_BITS = 10240
+# Algorithmic bytes: reference two-array flooding formulation
+# with binary64 messages. Per executed iteration: read+write b2c, read+write c2b
+# (4 E w) plus the LLR read (N w); per frame: Bob's bits in, decoded bits out,
+# syndrome in (2N + M bytes).
+E_EDGES, M_CHECKS, W = 30720, 5231, 8
+B_ITER = 4 * E_EDGES * W + N_BITS * W          # 1,064,960
+B_FRAME = 2 * N_BITS + M_CHECKS                 # 25,711
+HBM_PEAK_GBS = 8000.0                           # MI355X_MICROARCH.md, HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=4096)
+    ap.add_argument("--qber", type=float, default=0.02)
+    ap.add_argument("--max-iters", type=int, default=50)
+    ap.add_argument("--threshold", type=float, default=100.0)
+    ap.add_argument("--seed", type=int, default=777)
+    ap.add_argument("--cpu-frames", type=int, default=4096,
+                    help="frames in the CPU-baseline sample (0 disables)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def load_code(device):
+    import qkd_ldpc_amd as Q
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "code_n10240.npz")))
+    return Q.HMatrix.from_check_lists(int(g["dims"][0]), g["chk_off"], g["chk_idx"],
+                                      device=device), g
+
+
+def pmc_traffic():
+    """HBM bytes per decode launch from the newest profiles/*pmc*.json written by
+    tools/pmc_traffic.py (separate rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_decode*.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
+def cpu_baseline(args, g):
+    """The oracle (CPU restatement of the reference, glibc libm, -O3) on a bounded
+    sample of the same workload, one frame per task on `threads` host threads."""
+    from oracle import oracle as O
+    O.build()
+    code = O.Code.from_lists(g)
+    frames = args.cpu_frames
+    seeds = O.seeds(args.seed, frames)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    r = code.trials(args.qber, seeds, 0, args.max_iters, args.threshold, True, threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": frames * N_BITS / dt,
+        "unit": "bit/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{frames} frames of the same config (seeds 777[0:{frames}]), "
+                  f"{threads} threads, {dt:.2f} s wall, mean it "
+                  f"{float(np.mean(r['iters'])):.4f}",
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import qkd_ldpc_amd as Q
+
+    H, g = load_code(torch.cuda.current_device())
+    dev = torch.device("cuda", torch.cuda.current_device())
+    F = args.frames
+    all_seeds = Q.make_seeds(args.seed, F * world)
+    seeds = torch.from_numpy(all_seeds[rank * F:(rank + 1) * F].view(np.int64)).to(dev)
+    ws = Q.Workspace(H)
+    stream = torch.cuda.current_stream()
+
+    # key pairs resident in HBM before the timed region
+    alice, bob, exact_q = Q.keygen(H, seeds, args.qber, 0, workspace=ws)
+    q = float(exact_q[0].item())
+    iters = torch.empty(F, dtype=torch.int32, device=dev)
+    sp = torch.empty(F, dtype=torch.uint8, device=dev)
+    ko = torch.empty(F, dtype=torch.uint8, device=dev)
+    counters = torch.empty(Q._native.COUNTERS_BYTES, dtype=torch.uint8, device=dev)
+    cnt_u64 = counters.view(torch.int64)
+    L = Q._native.lib()
+    sptr = int(stream.cuda_stream)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        Q._native.check(L.qkd_qkd_ldpc_batch(H.handle, ws.handle, alice.data_ptr(), bob.data_ptr(), F,
+                                             q, args.max_iters, args.threshold, Q.FLAG_THRESHOLD,
+                                             None, iters.data_ptr(), sp.data_ptr(), ko.data_ptr(), sptr))
+        if ev is not None:
+            ev[1].record(stream)
+        Q._native.check(L.qkd_counters_batch(iters.data_ptr(), sp.data_ptr(), ko.data_ptr(), F,
+                                             counters.data_ptr(), H.device, sptr))
+        if world > 1:
+            dist.all_reduce(cnt_u64[:5], op=dist.ReduceOp.SUM)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+
+    c = Q.read_counters(counters)
+    it_np = iters.cpu().numpy()
+    frames_total = F * world
+    value = frames_total * N_BITS * args.steps / elapsed
+    # per-launch algorithmic bytes on this rank (executed iterations)
+    sum_it_local = int(it_np.astype(np.int64).sum())
+    alg_bytes = sum_it_local * B_ITER + F * B_FRAME
+    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    achieved = alg_bytes / avg_kernel_s / 1e9
+    traffic, traffic_src = pmc_traffic()
+
+    stats = Q.counters_to_stats(c, frames_total, args.max_iters, q)
+    if rank == 0:
+        out = {
+            "metric": "decoded key bits/sec + FER, N=10240 R=0.49 @ QBER=0.02, 50 iters",
+            "value": value,
+            "unit": "bit/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: reference keygen (xoshiro256++ seed 777, exact-QBER error "
+                    "injection) on the device; reference alist code N=10240",
+            "config": {
+                "workload": "configs[1]: alist (N=10240,M=5231,R=0.49,CW=3,SEED=666), "
+                            f"QBER {args.qber}, <= {args.max_iters} iterations, clamp "
+                            f"{args.threshold}, {F}-frame batch per GPU",
+                "frames_per_gpu": F,
+                "parallelism": f"frames sharded over {world} GPU(s), counters all-reduced",
+            },
+            "fer": stats["fer"],
+            "mean_iterations": stats["iterations_successful_sp_mean"],
+            "sum_iterations": stats["sum_iters_sp"],
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "decode_kernel (qkd_qkd_ldpc_batch, HIP events on its stream)",
+                "kernel_ms": avg_kernel_s * 1e3,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "traffic_source": traffic_src,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
+            out["cpu_baseline"] = cpu_baseline(args, g)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,188 @@
+/*
+ * qkd_ldpc.h — C ABI of the MI355X-native QKD LDPC sum-product decoder.
+ *
+ * Drop-in boundary for the hot path of ColdCloudd/QKD_LDPC (snapshot
+ * 2024-12-23). Every entry point below names the reference interface it
+ * replaces (file:line under the reference tree). Plain C types only: no HIP,
+ * no torch. Device pointers are raw addresses on the code's device; `stream`
+ * is a hipStream_t passed as void* (NULL = the null stream).
+ *
+ * Bit-exactness contract: for the same inputs, every per-frame output here
+ * (decoded bits, iteration count, syndrome match, key match, exact QBER) is
+ * identical to the reference's fp64 CPU path (glibc tanh/atanh, flooding
+ * schedule, reference accumulation order).
+ *
+ * Threading: a qkd_code is immutable after creation and may be shared by any
+ * number of host threads. Calls that need device scratch take a
+ * qkd_workspace*; pass NULL to use the code's internal workspace, which is
+ * guarded by a mutex and therefore serialises such calls at the host (calls
+ * on different streams then must not overlap on the device: they are
+ * ordered by an internal event). For concurrent streams create one
+ * workspace per stream.
+ *
+ * Errors: no exception crosses this boundary. Every call returns a
+ * qkd_status; qkd_last_error() returns a thread-local message for the most
+ * recent failure on the calling thread. The reference signals the same
+ * conditions by throwing std::runtime_error (e.g.
+ * array_and_matrix_operations.cpp:116,159,223; simulation.cpp:174).
+ */
+#ifndef QKD_LDPC_H
+#define QKD_LDPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QKD_LDPC_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define QKD_API __attribute__((visibility("default")))
+#else
+#define QKD_API
+#endif
+
+typedef enum qkd_status {
+    QKD_OK = 0,
+    QKD_ERR_INVALID_ARG = 1,     /* null pointer, zero size, bad flag        */
+    QKD_ERR_BAD_CODE = 2,        /* adjacency out of range / inconsistent    */
+    QKD_ERR_UNSORTED = 3,        /* an adjacency row is not ascending: the
+                                    reference would silently route messages
+                                    to the wrong edges (A1 invariant)        */
+    QKD_ERR_QBER_TOO_SMALL = 4,  /* floor(N*q) == 0 (simulation.cpp:170-175) */
+    QKD_ERR_DEVICE = 5,          /* HIP runtime failure                      */
+    QKD_ERR_OUT_OF_MEMORY = 6,
+    QKD_ERR_IO = 7,              /* matrix file unreadable / malformed       */
+    QKD_ERR_UNSUPPORTED = 8      /* code shape outside what the kernels take */
+} qkd_status;
+
+/* Decoder flags (bitwise OR). */
+#define QKD_FLAG_THRESHOLD 0x1u  /* CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD
+                                    (qkd_ldpc_algorithm.cpp:246,313)         */
+
+typedef struct qkd_code qkd_code;
+typedef struct qkd_workspace qkd_workspace;
+
+typedef struct qkd_code_info {
+    int32_t n_bits;              /* H_matrix::num_bit_nodes                  */
+    int32_t n_checks;            /* H_matrix::num_check_nodes                */
+    int32_t n_edges;
+    int32_t max_bit_degree;      /* H_matrix::max_bit_nodes_weight           */
+    int32_t max_check_degree;    /* H_matrix::max_check_nodes_weight         */
+    int32_t is_regular;          /* H_matrix::is_regular                     */
+    int32_t device;
+} qkd_code_info;
+
+/* Per-QBER-point reduction of a trial batch (simulation.cpp:252-312): only
+ * frames whose syndrome matched contribute to the iteration statistics, and
+ * ldpc_ok counts key matches among them. */
+typedef struct qkd_counters {
+    uint64_t frames;
+    uint64_t sp_ok;              /* trials_successful_sp                     */
+    uint64_t ldpc_ok;            /* trials_successful_ldpc                   */
+    uint64_t sum_iters;          /* sum of iterations over sp_ok frames      */
+    uint64_t sum_iters_sq;       /* sum of squares, same frames              */
+    uint32_t min_iters;          /* over sp_ok frames (UINT32_MAX if none)   */
+    uint32_t max_iters;          /* over sp_ok frames (0 if none)            */
+} qkd_counters;
+
+/* ---- library ----------------------------------------------------------- */
+QKD_API int qkd_abi_version(void);
+QKD_API const char *qkd_last_error(void);
+QKD_API const char *qkd_status_string(qkd_status s);
+/* Number of visible HIP devices (0 when none; never fails). */
+QKD_API int qkd_device_count(void);
+
+/* ---- code object: replaces H_matrix + its readers -----------------------
+ * H_matrix (array_and_matrix_operations.hpp:16-27), read_sparse_alist_matrix
+ * (array_and_matrix_operations.cpp:109-292), read_dense_matrix (:295-421),
+ * free_matrix_H (:88-94).
+ * check_ptr[m+1] / check_idx[E]: 0-based CSR of check_nodes (bits of each
+ * check, each row ascending). The bit-side lists (bit_nodes) are derived.
+ * Validation: indices in range, no duplicate edge, rows ascending
+ * (QKD_ERR_UNSORTED otherwise). Device data is uploaded once. */
+QKD_API qkd_code *qkd_code_create(int32_t n_bits, int32_t n_checks, const int32_t *check_ptr,
+                          const int32_t *check_idx, int device, qkd_status *status);
+/* Reads an alist file with the reference reader's rules (weights line,
+ * non-zero counts per line, 1-based entries, the first `weight` entries
+ * of each line). */
+QKD_API qkd_code *qkd_code_from_alist(const char *path, int device, qkd_status *status);
+/* Reads a dense 0/1 matrix file (one row per line). */
+QKD_API qkd_code *qkd_code_from_dense(const char *path, int device, qkd_status *status);
+QKD_API void qkd_code_destroy(qkd_code *code);
+QKD_API qkd_status qkd_code_get_info(const qkd_code *code, qkd_code_info *info);
+/* Host copies of the adjacency (any pointer may be NULL). bit_ptr[n+1],
+ * bit_idx[E] are the reference's bit_nodes rows (ascending checks). */
+QKD_API qkd_status qkd_code_get_adjacency(const qkd_code *code, int32_t *check_ptr, int32_t *check_idx,
+                                  int32_t *bit_ptr, int32_t *bit_idx);
+
+/* ---- workspace ------------------------------------------------------------ */
+QKD_API qkd_workspace *qkd_workspace_create(const qkd_code *code, qkd_status *status);
+QKD_API void qkd_workspace_destroy(qkd_workspace *ws);
+
+/* ---- batched device entry points (all arrays device-resident) ------------ */
+
+/* calculate_syndrome_irregular / _regular (array_and_matrix_operations.cpp:463-486)
+ * bits[F*N] (0/1 bytes) -> syndrome[F*M] (0/1 bytes). */
+QKD_API qkd_status qkd_syndrome_batch(const qkd_code *code, const uint8_t *bits, size_t n_frames,
+                              uint8_t *syndrome, void *stream);
+
+/* sum_product_decoding_irregular / _regular (qkd_ldpc_algorithm.cpp:3-345):
+ * llr[F*N] fp64 channel LLRs, syndrome[F*M] 0/1 bytes -> bits_out[F*N] (last
+ * hard decision), iterations[F] (SP_result::iterations_num) and
+ * syndromes_match[F] (SP_result::syndromes_match). msg_threshold is
+ * CFG.SUM_PRODUCT_MSG_LLR_THRESHOLD, applied when QKD_FLAG_THRESHOLD is set.
+ * bits_out may be NULL. */
+QKD_API qkd_status qkd_decode_batch(const qkd_code *code, qkd_workspace *ws, const double *llr,
+                            const uint8_t *syndrome, size_t n_frames, uint32_t max_iterations,
+                            double msg_threshold, uint32_t flags, uint8_t *bits_out,
+                            uint32_t *iterations, uint8_t *syndromes_match, void *stream);
+
+/* QKD_LDPC_irregular / _regular (qkd_ldpc_algorithm.cpp:347-447), batched:
+ * LLR_i = bob_i ? -log((1-q)/q) : +log((1-q)/q), Alice's syndrome, decode,
+ * keys_match = (decoded == alice). alice/bob [F*N] 0/1 bytes; one QBER for
+ * the batch. bits_out may be NULL. */
+QKD_API qkd_status qkd_qkd_ldpc_batch(const qkd_code *code, qkd_workspace *ws, const uint8_t *alice,
+                              const uint8_t *bob, size_t n_frames, double qber,
+                              uint32_t max_iterations, double msg_threshold, uint32_t flags,
+                              uint8_t *bits_out, uint32_t *iterations, uint8_t *syndromes_match,
+                              uint8_t *keys_match, void *stream);
+
+/* generate_random_bit_array + introduce_errors (array_and_matrix_operations.cpp:424-460)
+ * for frame k seeded with seeds[k] + seed_offset (simulation.cpp:163,247),
+ * on the device. alice/bob [F*N] 0/1 bytes; exact_qber[F] may be NULL.
+ * Returns QKD_ERR_QBER_TOO_SMALL when floor(N*q_nominal) == 0. */
+QKD_API qkd_status qkd_keygen_batch(const qkd_code *code, qkd_workspace *ws, const uint64_t *seeds,
+                            uint64_t seed_offset, size_t n_frames, double q_nominal,
+                            uint8_t *alice, uint8_t *bob, double *exact_qber, void *stream);
+
+/* run_trial (simulation.cpp:161-189) for F frames, fused on the device:
+ * keygen -> LLR -> Alice syndrome -> decode -> key compare. Per-frame outputs
+ * (any may be NULL) and, if counters != NULL (device memory, one
+ * qkd_counters), the batch reduction of simulation.cpp:252-312. */
+QKD_API qkd_status qkd_trials_batch(const qkd_code *code, qkd_workspace *ws, const uint64_t *seeds,
+                            uint64_t seed_offset, size_t n_frames, double q_nominal,
+                            uint32_t max_iterations, double msg_threshold, uint32_t flags,
+                            uint32_t *iterations, uint8_t *syndromes_match, uint8_t *keys_match,
+                            double *exact_qber, qkd_counters *counters, void *stream);
+
+/* Reduction alone: per-frame results -> counters (device memory). */
+QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t *syndromes_match,
+                              const uint8_t *keys_match, size_t n_frames, qkd_counters *counters,
+                              int device, void *stream);
+
+/* ---- host helpers --------------------------------------------------------- */
+/* seeds[k] = k-th raw xoshiro256++(simulation_seed) output (simulation.cpp:222-228). */
+QKD_API qkd_status qkd_make_seeds(uint64_t simulation_seed, size_t count, uint64_t *seeds_host);
+/* get_rate_based_QBER_range (simulation.cpp:48-70) for one table row:
+ * writes min(capacity, steps) values, returns the step count in *count. */
+QKD_API qkd_status qkd_qber_range(double begin, double end, double step, double *values_host,
+                          size_t capacity, size_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QKD_LDPC_H */

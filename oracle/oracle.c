@@ -1,0 +1,506 @@
+/*
+ * oracle.c — CPU restatement of the reference QKD-LDPC hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This file is the checker that tests/, the smoke
+ * test in __graft_entry__.py and bench.py's `cpu_baseline` leg compare the HIP
+ * product against. Nothing in qkd_ldpc_amd/ links, loads or calls it.
+ *
+ * It restates, in plain C with glibc libm, the algorithm of ColdCloudd/QKD_LDPC
+ * (snapshot 2024-12-23). Each function cites the reference file:line it
+ * follows. The reference itself is not buildable in this image without
+ * stand-in headers for three absent dependencies (XoshiroCpp, BS::thread_pool,
+ * indicators), so per the build rules it is not compiled here; parity of this
+ * restatement is pinned instead against the reference outputs recorded in
+ * SURVEY.md §4/§6 (golden file tests/golden/reference_probe.json):
+ *   - the textbook known answers (N=6 regular, N=10 irregular);
+ *   - seeds[0] of xoshiro256++(777);
+ *   - per-half-iteration FNV-1a-style fingerprints of every message of frame 0
+ *     of config 2 (N=10240, seed 777, QBER 0.02);
+ *   - the config-2 aggregate statistics and the config-3 FER table.
+ *
+ * Third-party algorithms restated here (absent from /root/reference):
+ *   - XoshiroCpp 1.1 Xoshiro256PlusPlus: SplitMix64 seeding + xoshiro256++
+ *     (published algorithm, Blackman & Vigna).
+ *   - libstdc++ (GCC 11.4) uniform_int_distribution (Lemire _S_nd with a
+ *     128-bit product) and std::shuffle's two-swaps-per-draw loop.
+ *   - glibc 2.35 tanh/atanh/log: called directly (this is the real libm).
+ *
+ * Build: see oracle/Makefile (gcc -O3 -ffp-contract=off, -lm -lpthread).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* Parity-check matrix: the reference's H_matrix (array_and_matrix_operations.hpp:16-27)
+ * stored as two jagged adjacency lists flattened into offset arrays. Row order
+ * and entry order are exactly as read (the reference never sorts).            */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int n, m;                   /* num_bit_nodes, num_check_nodes            */
+    int max_dv, max_dc;         /* max_bit/check_nodes_weight                */
+    int is_regular;
+    int *bit_off, *bit_idx;     /* bit_nodes[i]  = bit_idx[bit_off[i] ..]    */
+    int *chk_off, *chk_idx;     /* check_nodes[j]= chk_idx[chk_off[j] ..]    */
+} orc_code;
+
+ORC_API void orc_code_free(orc_code *h) {
+    if (!h) return;
+    free(h->bit_off); free(h->bit_idx); free(h->chk_off); free(h->chk_idx);
+    free(h);
+}
+
+static orc_code *code_alloc(int n, int m, int e) {
+    orc_code *h = (orc_code *)calloc(1, sizeof(orc_code));
+    h->n = n; h->m = m;
+    h->bit_off = (int *)calloc((size_t)n + 1, sizeof(int));
+    h->chk_off = (int *)calloc((size_t)m + 1, sizeof(int));
+    h->bit_idx = (int *)calloc((size_t)(e > 0 ? e : 1), sizeof(int));
+    h->chk_idx = (int *)calloc((size_t)(e > 0 ? e : 1), sizeof(int));
+    return h;
+}
+
+/* Build from the two adjacency lists directly (0-based), as given. */
+ORC_API orc_code *orc_code_from_lists(int n, int m, const int *bit_off, const int *bit_idx,
+                                      const int *chk_off, const int *chk_idx,
+                                      int max_dv, int max_dc) {
+    int e = bit_off[n];
+    orc_code *h = code_alloc(n, m, e);
+    memcpy(h->bit_off, bit_off, sizeof(int) * ((size_t)n + 1));
+    memcpy(h->chk_off, chk_off, sizeof(int) * ((size_t)m + 1));
+    memcpy(h->bit_idx, bit_idx, sizeof(int) * (size_t)e);
+    memcpy(h->chk_idx, chk_idx, sizeof(int) * (size_t)chk_off[m]);
+    h->max_dv = max_dv; h->max_dc = max_dc;
+    int reg = 1;
+    for (int i = 0; i < n; i++) if (bit_off[i + 1] - bit_off[i] != bit_off[1] - bit_off[0]) reg = 0;
+    for (int j = 0; j < m; j++) if (chk_off[j + 1] - chk_off[j] != chk_off[1] - chk_off[0]) reg = 0;
+    h->is_regular = reg;
+    return h;
+}
+
+/* read_dense_matrix (array_and_matrix_operations.cpp:295-421): rows of 0/1.
+ * bit_nodes[i] = rows with a 1 in column i (ascending), check_nodes[j] =
+ * columns with a 1 in row j (ascending) — get_bit_nodes/get_check_nodes :4-47. */
+ORC_API orc_code *orc_code_from_dense(const uint8_t *dense, int m, int n) {
+    int e = 0;
+    for (int k = 0; k < m * n; k++) e += dense[k] != 0;
+    orc_code *h = code_alloc(n, m, e);
+    int p = 0;
+    for (int i = 0; i < n; i++) {
+        h->bit_off[i] = p;
+        for (int j = 0; j < m; j++) if (dense[(size_t)j * n + i]) h->bit_idx[p++] = j;
+    }
+    h->bit_off[n] = p;
+    p = 0;
+    for (int j = 0; j < m; j++) {
+        h->chk_off[j] = p;
+        for (int i = 0; i < n; i++) if (dense[(size_t)j * n + i]) h->chk_idx[p++] = i;
+    }
+    h->chk_off[m] = p;
+    int mdv = 0, mdc = 0, reg = 1;
+    for (int i = 0; i < n; i++) {
+        int d = h->bit_off[i + 1] - h->bit_off[i];
+        if (d > mdv) mdv = d;
+        if (d != h->bit_off[1] - h->bit_off[0]) reg = 0;
+    }
+    for (int j = 0; j < m; j++) {
+        int d = h->chk_off[j + 1] - h->chk_off[j];
+        if (d > mdc) mdc = d;
+        if (d != h->chk_off[1] - h->chk_off[0]) reg = 0;
+    }
+    h->max_dv = mdv; h->max_dc = mdc; h->is_regular = reg;
+    return h;
+}
+
+/* read_sparse_alist_matrix (array_and_matrix_operations.cpp:109-292). Each
+ * line is read as whitespace-separated ints up to the first non-int token
+ * (the istringstream >> int loop, :134-145). Row i of bit_nodes takes the
+ * FIRST weight[i] numbers of its line minus one (:250-257), after checking
+ * that the line holds exactly weight[i] non-zero entries (:208-243).
+ * Returns NULL and writes a message on any validation failure.             */
+typedef struct { int *v; int n, cap; } ivec;
+
+static int parse_line(const char *s, ivec *out) {
+    out->n = 0;
+    for (;;) {
+        char *end;
+        while (*s == ' ' || *s == '\t' || *s == '\r' || *s == '\v' || *s == '\f') s++;
+        if (!*s || *s == '\n') break;
+        long x = strtol(s, &end, 10);
+        if (end == s) break;
+        if (out->n == out->cap) {
+            out->cap = out->cap ? out->cap * 2 : 16;
+            out->v = (int *)realloc(out->v, sizeof(int) * (size_t)out->cap);
+        }
+        out->v[out->n++] = (int)x;
+        s = end;
+    }
+    return out->n;
+}
+
+ORC_API orc_code *orc_code_from_alist(const char *path, char *err, int errlen) {
+    FILE *fp = fopen(path, "r");
+    if (!fp) { snprintf(err, (size_t)errlen, "Failed to open file: %s", path); return NULL; }
+    ivec *lines = NULL;
+    int nl = 0, capl = 0;
+    char *buf = NULL;
+    size_t bcap = 0;
+    ssize_t len;
+    while ((len = getline(&buf, &bcap, fp)) >= 0) {
+        if (nl == capl) {
+            capl = capl ? capl * 2 : 1024;
+            lines = (ivec *)realloc(lines, sizeof(ivec) * (size_t)capl);
+        }
+        memset(&lines[nl], 0, sizeof(ivec));
+        parse_line(buf, &lines[nl]);
+        nl++;
+    }
+    free(buf);
+    fclose(fp);
+    orc_code *h = NULL;
+    if (nl == 0) { snprintf(err, (size_t)errlen, "File is empty"); goto done; }
+    if (nl < 4) { snprintf(err, (size_t)errlen, "Insufficient data in the file"); goto done; }
+    if (lines[0].n != 2 || lines[1].n != 2) { snprintf(err, (size_t)errlen, "File format does not match the alist format"); goto done; }
+    int n = lines[0].v[0], m = lines[0].v[1];
+    int nb = lines[2].n, nc = lines[3].n;
+    if (nl < 4 + nb + nc) { snprintf(err, (size_t)errlen, "Insufficient data in the file"); goto done; }
+    if (n != nb || m != nc) { snprintf(err, (size_t)errlen, "Dimension/weight-line length mismatch"); goto done; }
+    for (int i = 0; i < nb + nc; i++) {
+        const ivec *L = &lines[4 + i];
+        int w = i < nb ? lines[2].v[i] : lines[3].v[i - nb];
+        int nz = 0;
+        for (int k = 0; k < L->n; k++) nz += L->v[k] != 0;
+        if (nz != w || w > L->n) { snprintf(err, (size_t)errlen, "Non-zero count mismatch on line %d", 5 + i); goto done; }
+    }
+    int e_b = 0, e_c = 0;
+    for (int i = 0; i < nb; i++) e_b += lines[2].v[i];
+    for (int j = 0; j < nc; j++) e_c += lines[3].v[j];
+    h = code_alloc(n, m, e_b > e_c ? e_b : e_c);
+    int p = 0;
+    for (int i = 0; i < n; i++) {
+        h->bit_off[i] = p;
+        for (int k = 0; k < lines[2].v[i]; k++) h->bit_idx[p++] = lines[4 + i].v[k] - 1;
+    }
+    h->bit_off[n] = p;
+    p = 0;
+    for (int j = 0; j < m; j++) {
+        h->chk_off[j] = p;
+        for (int k = 0; k < lines[3].v[j]; k++) h->chk_idx[p++] = lines[4 + n + j].v[k] - 1;
+    }
+    h->chk_off[m] = p;
+    h->max_dv = lines[1].v[0];
+    h->max_dc = lines[1].v[1];
+    int reg = 1;
+    for (int i = 0; i < n; i++) if (lines[2].v[i] != lines[2].v[0]) reg = 0;
+    for (int j = 0; j < m; j++) if (lines[3].v[j] != lines[3].v[0]) reg = 0;
+    h->is_regular = reg;
+done:
+    for (int i = 0; i < nl; i++) free(lines[i].v);
+    free(lines);
+    return h;
+}
+
+ORC_API void orc_code_lists(const orc_code *h, int *bit_off, int *bit_idx, int *chk_off, int *chk_idx) {
+    memcpy(bit_off, h->bit_off, sizeof(int) * ((size_t)h->n + 1));
+    memcpy(chk_off, h->chk_off, sizeof(int) * ((size_t)h->m + 1));
+    memcpy(bit_idx, h->bit_idx, sizeof(int) * (size_t)h->bit_off[h->n]);
+    memcpy(chk_idx, h->chk_idx, sizeof(int) * (size_t)h->chk_off[h->m]);
+}
+
+ORC_API void orc_code_dims(const orc_code *h, int *out6) {
+    out6[0] = h->n; out6[1] = h->m; out6[2] = h->bit_off[h->n];
+    out6[3] = h->max_dv; out6[4] = h->max_dc; out6[5] = h->is_regular;
+}
+
+/* ------------------------------------------------------------------------ */
+/* RNG: XoshiroCpp::Xoshiro256PlusPlus(seed) and libstdc++ GCC-11 distributions */
+/* ------------------------------------------------------------------------ */
+typedef struct { uint64_t s[4]; } orc_rng;
+
+static inline uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+ORC_API void orc_rng_seed(orc_rng *r, uint64_t seed) {
+    uint64_t z = seed;                          /* SplitMix64 state */
+    for (int i = 0; i < 4; i++) {
+        z += 0x9e3779b97f4a7c15ull;
+        uint64_t v = z;
+        v = (v ^ (v >> 30)) * 0xbf58476d1ce4e5b9ull;
+        v = (v ^ (v >> 27)) * 0x94d049bb133111ebull;
+        r->s[i] = v ^ (v >> 31);
+    }
+}
+
+ORC_API uint64_t orc_rng_next(orc_rng *r) {
+    uint64_t *s = r->s;
+    uint64_t res = rotl64(s[0] + s[3], 23) + s[0];
+    uint64_t t = s[1] << 17;
+    s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3];
+    s[2] ^= t;
+    s[3] = rotl64(s[3], 45);
+    return res;
+}
+
+/* uniform_int_distribution<>{0, range-1} for a 64-bit URBG: Lemire _S_nd. */
+static inline uint64_t lemire(orc_rng *r, uint64_t range) {
+    unsigned __int128 prod = (unsigned __int128)orc_rng_next(r) * range;
+    uint64_t low = (uint64_t)prod;
+    if (low < range) {
+        uint64_t thr = (0 - range) % range;
+        while (low < thr) {
+            prod = (unsigned __int128)orc_rng_next(r) * range;
+            low = (uint64_t)prod;
+        }
+    }
+    return (uint64_t)(prod >> 64);
+}
+
+/* QKD_LDPC_batch_simulation seeds (simulation.cpp:222-228): full-range
+ * uniform_int_distribution<size_t> returns the raw draw. */
+ORC_API void orc_seeds(uint64_t sim_seed, size_t count, uint64_t *out) {
+    orc_rng r;
+    orc_rng_seed(&r, sim_seed);
+    for (size_t i = 0; i < count; i++) out[i] = orc_rng_next(&r);
+}
+
+/* generate_random_bit_array (array_and_matrix_operations.cpp:424-431). */
+static void gen_bits(orc_rng *r, int n, int *out) {
+    for (int i = 0; i < n; i++) out[i] = (int)lemire(r, 2);
+}
+
+/* introduce_errors (array_and_matrix_operations.cpp:434-460) with GCC-11
+ * std::shuffle over size_t positions. Returns the exact QBER. */
+static double introduce_errors(orc_rng *r, const int *in, int n, double q, int *out, size_t *pos) {
+    size_t ne = (size_t)((double)n * q);   /* static_cast<size_t>(length * p) */
+    memcpy(out, in, sizeof(int) * (size_t)n);
+    if (ne == 0) return 0.0;
+    for (int i = 0; i < n; i++) pos[i] = (size_t)i;
+    if (n > 1) {
+        size_t i = 1;
+        if ((n % 2) == 0) {                /* even count: one lone swap first */
+            size_t x = (size_t)lemire(r, 2);
+            size_t t = pos[i]; pos[i] = pos[x]; pos[x] = t;
+            i++;
+        }
+        while (i != (size_t)n) {
+            uint64_t b0 = i + 1, b1 = i + 2;
+            uint64_t x = lemire(r, b0 * b1);
+            size_t a = (size_t)(x / b1), b = (size_t)(x % b1);
+            size_t t = pos[i]; pos[i] = pos[a]; pos[a] = t; i++;
+            t = pos[i]; pos[i] = pos[b]; pos[b] = t; i++;
+        }
+    }
+    for (size_t k = 0; k < ne; k++) out[pos[k]] ^= 1;
+    return (double)ne / (double)n;
+}
+
+/* Alice/Bob key pair for one trial (simulation.cpp:163-168). */
+ORC_API double orc_keygen(uint64_t seed, int n, double q_nom, int *alice, int *bob) {
+    orc_rng r;
+    orc_rng_seed(&r, seed);
+    size_t *pos = (size_t *)malloc(sizeof(size_t) * (size_t)n);
+    gen_bits(&r, n, alice);
+    double q = introduce_errors(&r, alice, n, q_nom, bob, pos);
+    free(pos);
+    return q;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Matrix / array helpers (array_and_matrix_operations.cpp)                 */
+/* ------------------------------------------------------------------------ */
+/* calculate_syndrome_irregular :476-486 (the regular twin :463-473 is the same
+ * loop with max_check_nodes_weight bounds). */
+ORC_API void orc_syndrome(const orc_code *h, const int *bits, int *syn) {
+    for (int j = 0; j < h->m; j++) {
+        int s = 0;
+        for (int k = h->chk_off[j]; k < h->chk_off[j + 1]; k++) s ^= bits[h->chk_idx[k]];
+        syn[j] = s;
+    }
+}
+
+/* threshold_matrix_irregular :508-524 — compare-based, NaN passes through. */
+static void clamp_msgs(double *v, int cnt, double thr) {
+    for (int k = 0; k < cnt; k++) {
+        if (v[k] > thr) v[k] = thr;
+        else if (v[k] < -thr) v[k] = -thr;
+    }
+}
+
+static uint64_t fnv_doubles(const double *v, int cnt) {
+    uint64_t hsh = 0xcbf29ce484222325ull;
+    for (int k = 0; k < cnt; k++) {
+        uint64_t u;
+        memcpy(&u, &v[k], 8);
+        hsh = (hsh ^ u) * 0x100000001b3ull;
+    }
+    return hsh;
+}
+
+/* ------------------------------------------------------------------------ */
+/* sum_product_decoding_irregular (qkd_ldpc_algorithm.cpp:175-345).
+ * b2c is stored check-major (row j holds chk_off[j+1]-chk_off[j] slots), c2b
+ * bit-major (row i holds bit_off[i+1]-bit_off[i] slots), exactly the jagged
+ * layout of the reference; slot counters reproduce its message routing.
+ * `fp` (optional) receives the FNV fingerprint of c2b after each check phase
+ * clamp and of b2c after each bit phase clamp, interleaved: c2b#1, b2c#1, ...
+ * `ltrace` (optional, max_it*n) receives total_bit_llr per iteration.
+ * The regular twin (:3-173) iterates max_*_weight slots; for a regular matrix
+ * that is the same loop, which orc_decode asserts.                           */
+/* ------------------------------------------------------------------------ */
+ORC_API int orc_decode(const orc_code *h, const double *llr, const int *syndrome,
+                       int max_it, double thr, int thr_enable, int *out,
+                       int *iters, int *sp_ok, uint64_t *fp, int *n_fp, double *ltrace,
+                       double *max_llr) {
+    const int n = h->n, m = h->m, e = h->chk_off[m];
+    double *b2c = (double *)malloc(sizeof(double) * (size_t)(e ? e : 1));
+    double *c2b = (double *)malloc(sizeof(double) * (size_t)(h->bit_off[n] ? h->bit_off[n] : 1));
+    int *cpos = (int *)malloc(sizeof(int) * (size_t)n);
+    int *bpos = (int *)malloc(sizeof(int) * (size_t)m);
+    double *total = (double *)malloc(sizeof(double) * (size_t)n);
+    int *dsyn = (int *)malloc(sizeof(int) * (size_t)m);
+    int nfp = 0;
+    if (max_llr) *max_llr = 0.;
+
+    for (int k = 0; k < e; k++) b2c[k] = llr[h->chk_idx[k]];             /* :186-189 */
+
+    int it;
+    int done = 0;
+    for (it = 0; it < max_it; it++) {
+        for (int k = 0; k < e; k++) b2c[k] = tanh(b2c[k] / 2.);            /* :220-226 */
+        memset(cpos, 0, sizeof(int) * (size_t)n);
+        for (int j = 0; j < m; j++) {                                      /* :229-244 */
+            double row = syndrome[j] ? -1. : 1.;
+            for (int k = h->chk_off[j]; k < h->chk_off[j + 1]; k++) row *= b2c[k];
+            for (int k = h->chk_off[j]; k < h->chk_off[j + 1]; k++) {
+                double prod = row / b2c[k];
+                int bit = h->chk_idx[k];
+                c2b[h->bit_off[bit] + cpos[bit]] = 2. * atanh(prod);
+                cpos[bit]++;
+            }
+        }
+        if (thr_enable) clamp_msgs(c2b, h->bit_off[n], thr);                /* :246-249 */
+        if (fp) fp[nfp] = fnv_doubles(c2b, h->bit_off[n]);
+        nfp++;
+        for (int i = 0; i < n; i++) {                                      /* :256-267 */
+            double acc = llr[i];
+            for (int k = h->bit_off[i]; k < h->bit_off[i + 1]; k++) acc = acc + c2b[k];
+            total[i] = acc;
+            out[i] = (acc <= 0) ? 1 : 0;
+        }
+        if (ltrace) memcpy(ltrace + (size_t)it * n, total, sizeof(double) * (size_t)n);
+        orc_syndrome(h, out, dsyn);                                        /* :277 */
+        int eq = 1;
+        for (int j = 0; j < m; j++) if (dsyn[j] != syndrome[j]) { eq = 0; break; }
+        if (eq) { done = 1; break; }                                       /* :285-298 */
+        memset(bpos, 0, sizeof(int) * (size_t)m);
+        for (int i = 0; i < n; i++) {                                      /* :300-311 */
+            double col = total[i];
+            for (int k = h->bit_off[i]; k < h->bit_off[i + 1]; k++) {
+                double sum = col - c2b[k];
+                int chk = h->bit_idx[k];
+                b2c[h->chk_off[chk] + bpos[chk]] = sum;
+                bpos[chk]++;
+            }
+        }
+        if (thr_enable) clamp_msgs(b2c, e, thr);                            /* :313-316 */
+        if (fp) fp[nfp] = fnv_doubles(b2c, e);
+        nfp++;
+        if (max_llr) {                          /* TRACE_SUM_PRODUCT_LLR, :322-327 */
+            for (int k = 0; k < h->bit_off[n]; k++) if (fabs(c2b[k]) > *max_llr) *max_llr = fabs(c2b[k]);
+            for (int k = 0; k < e; k++) if (fabs(b2c[k]) > *max_llr) *max_llr = fabs(b2c[k]);
+        }
+    }
+    *iters = done ? it + 1 : max_it;
+    *sp_ok = done;
+    if (n_fp) *n_fp = nfp;
+    free(b2c); free(c2b); free(cpos); free(bpos); free(total); free(dsyn);
+    return 0;
+}
+
+/* QKD_LDPC_irregular (qkd_ldpc_algorithm.cpp:398-447): LLR init from Bob's key
+ * and the exact QBER, Alice syndrome, decode, key comparison. */
+ORC_API int orc_qkd_ldpc(const orc_code *h, const int *alice, const int *bob, double q,
+                         int max_it, double thr, int thr_enable,
+                         int *iters, int *sp_ok, int *key_ok, int *out) {
+    const int n = h->n;
+    double log_p = log((1. - q) / q);                                      /* :400 */
+    double *llr = (double *)malloc(sizeof(double) * (size_t)n);
+    int *syn = (int *)malloc(sizeof(int) * (size_t)h->m);
+    int *dec = out ? out : (int *)malloc(sizeof(int) * (size_t)n);
+    for (int i = 0; i < n; i++) llr[i] = bob[i] ? -log_p : log_p;          /* :402-405 */
+    orc_syndrome(h, alice, syn);                                           /* :413-414 */
+    orc_decode(h, llr, syn, max_it, thr, thr_enable, dec, iters, sp_ok, NULL, NULL, NULL, NULL);
+    int eq = 1;
+    for (int i = 0; i < n; i++) if (alice[i] != dec[i]) { eq = 0; break; } /* :433 */
+    *key_ok = eq;
+    free(llr); free(syn);
+    if (!out) free(dec);
+    return 0;
+}
+
+/* run_trial (simulation.cpp:161-189). Returns -1 when the key is too short
+ * for the QBER (the reference throws std::runtime_error, :170-175). */
+ORC_API int orc_run_trial(const orc_code *h, double q_nom, uint64_t seed, int max_it,
+                          double thr, int thr_enable, int *iters, int *sp_ok, int *key_ok,
+                          double *exact_q) {
+    const int n = h->n;
+    int *alice = (int *)malloc(sizeof(int) * (size_t)n);
+    int *bob = (int *)malloc(sizeof(int) * (size_t)n);
+    double q = orc_keygen(seed, n, q_nom, alice, bob);
+    *exact_q = q;
+    int rc = 0;
+    if (q == 0.) rc = -1;
+    else orc_qkd_ldpc(h, alice, bob, q, max_it, thr, thr_enable, iters, sp_ok, key_ok, NULL);
+    free(alice); free(bob);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Trial fan-out (the BS::thread_pool detach_loop of simulation.cpp:244-250):
+ * frame k runs run_trial(seed = seeds[k] + offset) on one of `threads`
+ * workers; per-frame results land in disjoint slots.                        */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const orc_code *h; double q; const uint64_t *seeds; uint64_t offset; size_t f;
+    int max_it; double thr; int thr_enable;
+    int *iters, *sp_ok, *key_ok; double *exact_q;
+    size_t next; pthread_mutex_t mu; int err;
+} trials_job;
+
+static void *trials_worker(void *arg) {
+    trials_job *j = (trials_job *)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        size_t k = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (k >= j->f) break;
+        int it = 0, sp = 0, ko = 0;
+        double q = 0;
+        if (orc_run_trial(j->h, j->q, j->seeds[k] + j->offset, j->max_it, j->thr, j->thr_enable,
+                          &it, &sp, &ko, &q) != 0) j->err = 1;
+        j->iters[k] = it; j->sp_ok[k] = sp; j->key_ok[k] = ko; j->exact_q[k] = q;
+    }
+    return NULL;
+}
+
+ORC_API int orc_trials(const orc_code *h, double q_nom, const uint64_t *seeds, uint64_t offset,
+                       size_t f, int max_it, double thr, int thr_enable, int threads,
+                       int *iters, int *sp_ok, int *key_ok, double *exact_q) {
+    trials_job j;
+    memset(&j, 0, sizeof(j));
+    j.h = h; j.q = q_nom; j.seeds = seeds; j.offset = offset; j.f = f;
+    j.max_it = max_it; j.thr = thr; j.thr_enable = thr_enable;
+    j.iters = iters; j.sp_ok = sp_ok; j.key_ok = key_ok; j.exact_q = exact_q;
+    pthread_mutex_init(&j.mu, NULL);
+    if (threads < 1) threads = 1;
+    pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    for (int t = 0; t < threads; t++) pthread_create(&tid[t], NULL, trials_worker, &j);
+    for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    free(tid);
+    pthread_mutex_destroy(&j.mu);
+    return j.err ? -1 : 0;
+}

@@ -1,0 +1,337 @@
+"""qkd_ldpc_amd — MI355X-native QKD LDPC sum-product decoding.
+
+Python view of the C ABI (include/qkd_ldpc.h). It mirrors the reference's
+hot-path interface (ColdCloudd/QKD_LDPC, src/qkd_ldpc_algorithm.hpp and
+src/array_and_matrix_operations.hpp) with batched, device-resident arrays:
+
+  reference (one frame, host int arrays)         here (F frames, torch tensors on the GPU)
+  ---------------------------------------------  ------------------------------------------
+  H_matrix + read_sparse_alist_matrix             HMatrix.from_alist(path)
+  read_dense_matrix                               HMatrix.from_dense(path)
+  calculate_syndrome_irregular/_regular           calculate_syndrome(H, bits)
+  sum_product_decoding_irregular/_regular         sum_product_decoding(H, llr, syndrome, ...)
+  QKD_LDPC_irregular/_regular                     qkd_ldpc(H, alice, bob, qber, ...)
+  generate_random_bit_array + introduce_errors    keygen(H, seeds, q_nominal, ...)
+  run_trial over a batch + the batch reduction    run_trials(H, seeds, q_nominal, ...)
+  seeds of QKD_LDPC_batch_simulation              make_seeds(simulation_seed, count)
+  get_rate_based_QBER_range (one table row)       qber_range(begin, end, step)
+
+Errors surface as QkdError (a RuntimeError, as the reference throws
+std::runtime_error). Every call runs HIP kernels; nothing falls back to CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+from ._native import FLAG_THRESHOLD, QkdError
+
+try:
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+__all__ = [
+    "HMatrix", "QkdError", "calculate_syndrome", "sum_product_decoding",
+    "sum_product_decoding_irregular", "sum_product_decoding_regular", "qkd_ldpc",
+    "QKD_LDPC_irregular", "QKD_LDPC_regular", "keygen", "run_trials", "make_seeds",
+    "qber_range", "Workspace", "counters_to_stats",
+]
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    return int(t.data_ptr())
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        return int(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)
+
+
+def _need_cuda(t, dtype, name):
+    if not (t.is_cuda and t.dtype == dtype and t.is_contiguous()):
+        raise QkdError(N.ERR_INVALID_ARG, f"{name} must be a contiguous {dtype} CUDA tensor")
+
+
+class HMatrix:
+    """The parity-check matrix (reference H_matrix, array_and_matrix_operations.hpp:16-27),
+    uploaded once to one device and immutable afterwards."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+        info = N.CodeInfo()
+        N.check(N.lib().qkd_code_get_info(self._h, C.byref(info)))
+        self.num_bit_nodes = info.n_bits
+        self.num_check_nodes = info.n_checks
+        self.n_edges = info.n_edges
+        self.max_bit_nodes_weight = info.max_bit_degree
+        self.max_check_nodes_weight = info.max_check_degree
+        self.is_regular = bool(info.is_regular)
+        self.device = info.device
+
+    # --- constructors (reference readers) ----------------------------------
+    @classmethod
+    def _make(cls, fn, *args):
+        st = C.c_int(0)
+        h = fn(*args, C.byref(st))
+        if not h:
+            raise QkdError(st.value, N.last_error())
+        return cls(h)
+
+    @classmethod
+    def from_alist(cls, path: str, device: int = 0) -> "HMatrix":
+        return cls._make(N.lib().qkd_code_from_alist, str(path).encode(), device)
+
+    @classmethod
+    def from_dense(cls, path: str, device: int = 0) -> "HMatrix":
+        return cls._make(N.lib().qkd_code_from_dense, str(path).encode(), device)
+
+    @classmethod
+    def from_check_lists(cls, n_bits: int, check_ptr, check_idx, device: int = 0) -> "HMatrix":
+        cp = np.ascontiguousarray(check_ptr, dtype=np.int32)
+        ci = np.ascontiguousarray(check_idx, dtype=np.int32)
+        return cls._make(N.lib().qkd_code_create, n_bits, cp.size - 1, cp.ctypes.data,
+                         ci.ctypes.data, device)
+
+    @classmethod
+    def from_dense_array(cls, dense, device: int = 0) -> "HMatrix":
+        d = np.asarray(dense)
+        ptr, idx = [0], []
+        for row in d:
+            idx.extend(np.nonzero(row)[0].tolist())
+            ptr.append(len(idx))
+        return cls.from_check_lists(d.shape[1], ptr, idx, device)
+
+    # --- adjacency ------------------------------------------------------------
+    def adjacency(self):
+        n, m, e = self.num_bit_nodes, self.num_check_nodes, self.n_edges
+        cp = np.zeros(m + 1, np.int32)
+        ci = np.zeros(e, np.int32)
+        bp = np.zeros(n + 1, np.int32)
+        bi = np.zeros(e, np.int32)
+        N.check(N.lib().qkd_code_get_adjacency(self._h, cp.ctypes.data, ci.ctypes.data,
+                                               bp.ctypes.data, bi.ctypes.data))
+        return cp, ci, bp, bi
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            N.lib().qkd_code_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Workspace:
+    """Device scratch for one stream (qkd_workspace)."""
+
+    def __init__(self, H: HMatrix):
+        st = C.c_int(0)
+        h = N.lib().qkd_workspace_create(H.handle, C.byref(st))
+        if not h:
+            raise QkdError(st.value, N.last_error())
+        self._h = C.c_void_p(h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            N.lib().qkd_workspace_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _ws(ws):
+    return ws.handle if ws is not None else None
+
+
+def calculate_syndrome(H: HMatrix, bits, stream=None):
+    """calculate_syndrome_irregular/_regular: bits [F, N] uint8 -> [F, M] uint8."""
+    _need_cuda(bits, torch.uint8, "bits")
+    f = bits.numel() // H.num_bit_nodes
+    out = torch.empty((f, H.num_check_nodes), dtype=torch.uint8, device=bits.device)
+    N.check(N.lib().qkd_syndrome_batch(H.handle, _ptr(bits), f, _ptr(out), _stream(stream)))
+    return out
+
+
+@dataclass
+class SPResult:
+    """SP_result (qkd_ldpc_algorithm.hpp:14-18), one entry per frame."""
+    iterations: "torch.Tensor"
+    syndromes_match: "torch.Tensor"
+    bits: "torch.Tensor | None"
+
+
+@dataclass
+class LDPCResult:
+    """LDPC_result (qkd_ldpc_algorithm.hpp:20-24), one entry per frame."""
+    iterations: "torch.Tensor"
+    syndromes_match: "torch.Tensor"
+    keys_match: "torch.Tensor"
+    bits: "torch.Tensor | None"
+
+
+def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
+                         msg_threshold: float = 100.0, threshold_enabled: bool = True,
+                         want_bits: bool = True, workspace=None, stream=None) -> SPResult:
+    """sum_product_decoding_irregular/_regular (qkd_ldpc_algorithm.cpp:3-345), batched.
+    llr [F, N] float64, syndrome [F, M] uint8 (0/1)."""
+    _need_cuda(llr, torch.float64, "llr")
+    _need_cuda(syndrome, torch.uint8, "syndrome")
+    f = llr.numel() // H.num_bit_nodes
+    dev = llr.device
+    bits = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev) if want_bits else None
+    iters = torch.empty(f, dtype=torch.int32, device=dev)
+    ok = torch.empty(f, dtype=torch.uint8, device=dev)
+    flags = FLAG_THRESHOLD if threshold_enabled else 0
+    N.check(N.lib().qkd_decode_batch(H.handle, _ws(workspace), _ptr(llr), _ptr(syndrome), f,
+                                     max_iterations, msg_threshold, flags, _ptr(bits), _ptr(iters),
+                                     _ptr(ok), _stream(stream)))
+    return SPResult(iters, ok, bits)
+
+
+# The reference has two twins that differ only in loop bounds; one kernel serves both.
+sum_product_decoding_irregular = sum_product_decoding
+sum_product_decoding_regular = sum_product_decoding
+
+
+def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
+             msg_threshold: float = 100.0, threshold_enabled: bool = True,
+             want_bits: bool = False, workspace=None, stream=None) -> LDPCResult:
+    """QKD_LDPC_irregular/_regular (qkd_ldpc_algorithm.cpp:347-447), batched.
+    alice, bob [F, N] uint8 (0/1); one QBER for the batch."""
+    _need_cuda(alice, torch.uint8, "alice")
+    _need_cuda(bob, torch.uint8, "bob")
+    f = alice.numel() // H.num_bit_nodes
+    dev = alice.device
+    bits = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev) if want_bits else None
+    iters = torch.empty(f, dtype=torch.int32, device=dev)
+    ok = torch.empty(f, dtype=torch.uint8, device=dev)
+    km = torch.empty(f, dtype=torch.uint8, device=dev)
+    flags = FLAG_THRESHOLD if threshold_enabled else 0
+    N.check(N.lib().qkd_qkd_ldpc_batch(H.handle, _ws(workspace), _ptr(alice), _ptr(bob), f, qber,
+                                       max_iterations, msg_threshold, flags, _ptr(bits),
+                                       _ptr(iters), _ptr(ok), _ptr(km), _stream(stream)))
+    return LDPCResult(iters, ok, km, bits)
+
+
+QKD_LDPC_irregular = qkd_ldpc
+QKD_LDPC_regular = qkd_ldpc
+
+
+def keygen(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0, workspace=None,
+           stream=None):
+    """generate_random_bit_array + introduce_errors for frames seeded seeds[k] + seed_offset.
+    Returns (alice [F,N] u8, bob [F,N] u8, exact_qber [F] f64) on the device."""
+    _need_cuda(seeds, torch.int64, "seeds")
+    f = seeds.numel()
+    dev = seeds.device
+    a = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    q = torch.empty(f, dtype=torch.float64, device=dev)
+    N.check(N.lib().qkd_keygen_batch(H.handle, _ws(workspace), _ptr(seeds), seed_offset, f,
+                                     q_nominal, _ptr(a), _ptr(b), _ptr(q), _stream(stream)))
+    return a, b, q
+
+
+@dataclass
+class TrialResults:
+    iterations: "torch.Tensor"
+    syndromes_match: "torch.Tensor"
+    keys_match: "torch.Tensor"
+    exact_qber: "torch.Tensor"
+    counters: "torch.Tensor"      # raw qkd_counters bytes (device)
+
+
+def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
+               max_iterations: int = 50, msg_threshold: float = 100.0,
+               threshold_enabled: bool = True, workspace=None, stream=None,
+               out: TrialResults | None = None) -> TrialResults:
+    """run_trial (simulation.cpp:161-189) for every frame, fused on the device, plus the
+    per-QBER-point counters of simulation.cpp:252-312. seeds: int64 CUDA tensor holding
+    the uint64 seed bits."""
+    _need_cuda(seeds, torch.int64, "seeds")
+    f = seeds.numel()
+    dev = seeds.device
+    if out is None:
+        out = TrialResults(torch.empty(f, dtype=torch.int32, device=dev),
+                           torch.empty(f, dtype=torch.uint8, device=dev),
+                           torch.empty(f, dtype=torch.uint8, device=dev),
+                           torch.empty(f, dtype=torch.float64, device=dev),
+                           torch.empty(N.COUNTERS_BYTES, dtype=torch.uint8, device=dev))
+    flags = FLAG_THRESHOLD if threshold_enabled else 0
+    N.check(N.lib().qkd_trials_batch(H.handle, _ws(workspace), _ptr(seeds), seed_offset, f,
+                                     q_nominal, max_iterations, msg_threshold, flags,
+                                     _ptr(out.iterations), _ptr(out.syndromes_match),
+                                     _ptr(out.keys_match), _ptr(out.exact_qber),
+                                     _ptr(out.counters), _stream(stream)))
+    return out
+
+
+def read_counters(counters) -> N.Counters:
+    raw = counters.detach().cpu().numpy().tobytes()
+    return N.Counters.from_buffer_copy(raw)
+
+
+def counters_to_stats(c: N.Counters, trials: int, max_iterations: int,
+                      initial_qber: float) -> dict:
+    """sim_result fields (simulation.hpp:29-43) from exact integer counters. The mean
+    and population std match the reference's two-pass double arithmetic to the
+    6 significant digits its CSV prints (simulation.cpp:285-312)."""
+    sp, ok = int(c.sp_ok), int(c.ldpc_ok)
+    mean = std = 0.0
+    mn, mx = max_iterations, 0
+    if sp > 0:
+        s1, s2 = int(c.sum_iters), int(c.sum_iters_sq)
+        mean = s1 / sp
+        std = ((sp * s2 - s1 * s1) / (sp * sp)) ** 0.5   # exact integer numerator
+        mn, mx = int(c.min_iters), int(c.max_iters)
+    return {
+        "initial_QBER": initial_qber,
+        "iterations_successful_sp_mean": mean,
+        "iterations_successful_sp_std_dev": std,
+        "iterations_successful_sp_min": 0 if mn == max_iterations else mn,
+        "iterations_successful_sp_max": mx,
+        "ratio_trials_successful_sp": sp / trials,
+        "ratio_trials_successful_ldpc": ok / trials,
+        "fer": 1.0 - ok / trials,
+        "sum_iters_sp": int(c.sum_iters),
+    }
+
+
+def make_seeds(simulation_seed: int, count: int) -> np.ndarray:
+    """seeds[k] = k-th raw xoshiro256++(simulation_seed) draw (simulation.cpp:222-228)."""
+    out = np.zeros(count, np.uint64)
+    N.check(N.lib().qkd_make_seeds(simulation_seed, count, out.ctypes.data))
+    return out
+
+
+def qber_range(begin: float, end: float, step: float) -> list[float]:
+    """One row of get_rate_based_QBER_range (simulation.cpp:48-70)."""
+    cnt = C.c_size_t(0)
+    N.check(N.lib().qkd_qber_range(begin, end, step, None, 0, C.byref(cnt)))
+    vals = np.zeros(max(cnt.value, 1), np.float64)
+    N.check(N.lib().qkd_qber_range(begin, end, step, vals.ctypes.data, cnt.value, C.byref(cnt)))
+    return vals[: cnt.value].tolist()

@@ -1,0 +1,682 @@
+// decode.hip — gfx950 kernels and launchers of the QKD LDPC decoder.
+//
+// Hot path: flooding sum-product decoding, reference
+// src/qkd_ldpc_algorithm.cpp:175-345 (irregular) / :3-173 (regular, the same
+// arithmetic for a regular code), reached through QKD_LDPC_* (:347-447) and
+// run_trial (src/simulation.cpp:161-189).
+//
+// MI355X mapping
+//   * One 1024-thread workgroup owns one frame at a time; workgroups are
+//     persistent (grid = resident workgroups) and pull frames from a device
+//     queue (one atomic per frame), so frames with 2 and 50 iterations mix
+//     without tail stalls.
+//   * Per-frame state is the reference's two message arrays collapsed to one:
+//     c2b messages (E binary64, slot-major per check, in HBM/L2/MALL) plus the
+//     bit totals (N binary64) in LDS. The reference's b2c message for edge
+//     (j,i) is exactly total_i - c2b(j,i) clamped (its :303-316), so it is
+//     recomputed inside the check update instead of being stored: same bits,
+//     half the message traffic.
+//   * Check phase: thread per check, slot-major coalesced c2b read/write, the
+//     d_c tanh values in registers, the extrinsic product by division (keeps
+//     the reference's 0/0 -> NaN behaviour). Bit phase: thread per bit,
+//     gathers its d_v c2b in ascending check order (the reference's
+//     std::accumulate order). Syndrome test: thread per check over LDS totals,
+//     block-wide OR.
+//   * tanh/atanh are the bit-exact restatements in qkd_math.h; the whole
+//     library builds with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "qkd_internal.h"
+#include "qkd_math.h"
+#include "qkd_rng.h"
+
+namespace qkd {
+
+enum DecodeMode : int {
+    kModeLlr = 0,  // qkd_decode_batch: caller LLRs + syndrome bytes
+    kModeKeys = 1  // QKD_LDPC path: packed alice/bob keys, LLR = +-log_p
+};
+
+struct DecodeArgs {
+    DeviceCode code;
+    uint32_t n_frames;
+    uint32_t max_it;
+    double thr;
+    int clamp_on;
+    // kModeLlr
+    const double* llr;
+    const uint8_t* syn;
+    // kModeKeys
+    const uint64_t* alice_w;
+    const uint64_t* bob_w;
+    uint32_t words;
+    double log_p;
+    // outputs
+    uint8_t* bits_out;
+    uint32_t* iters;
+    uint8_t* sp_ok;
+    uint8_t* key_ok;
+    // scratch
+    double* c2b;
+    size_t c2b_stride;
+    uint32_t* counter;
+};
+
+__device__ __forceinline__ double clamp_msg(double v, double thr) {
+    // threshold_matrix_irregular (array_and_matrix_operations.cpp:508-524):
+    // compare-based, so NaN passes through.
+    return v > thr ? thr : (v < -thr ? -thr : v);
+}
+
+// Block-wide any(); flags[2] live in LDS and alternate between calls. Every
+// call must be separated from the next by at least one __syncthreads().
+__device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) {
+    uint32_t* f = flags + (k & 1u);
+    const bool wave_hit = __any(p);
+    if (wave_hit && (threadIdx.x & 63) == 0) atomicOr(f, 1u);
+    __syncthreads();
+    const bool r = *f != 0;
+    if (threadIdx.x == 0) flags[(k + 1) & 1u] = 0;
+    k++;
+    return r;
+}
+
+// One check's update (qkd_ldpc_algorithm.cpp:220-249 for check j):
+//   b2c_k  = first ? LLR[bit_k] : clamp(total[bit_k] - c2b_k)      (:188, :303-316)
+//   t_k    = tanh(b2c_k / 2)                                       (:224)
+//   P      = (s_j ? -1 : 1) * t_0 * t_1 * ...   (left to right)    (:231-235)
+//   c2b_k  = clamp(2 * atanh(P / t_k))                             (:239-249)
+template <int DC>
+__device__ __forceinline__ void check_update(const DeviceCode& c, const double* total, double* c2b,
+                                             int j, int s, bool first, bool clamp_on, double thr) {
+    const int deg = c.chk_deg[j];
+    double t[DC];
+    double prod = s ? -1.0 : 1.0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k < deg) {
+            const int pos = k * c.m_pad + j;
+            const int bit = c.chk_bits[pos];
+            double b = total[bit];
+            if (!first) {
+                b = b - c2b[pos];
+                if (clamp_on) b = clamp_msg(b, thr);
+            }
+            t[k] = qkdm::tanh_ref(b / 2.0);
+            prod *= t[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k < deg) {
+            const int pos = k * c.m_pad + j;
+            double v = 2.0 * qkdm::atanh_ref(prod / t[k]);
+            if (clamp_on) v = clamp_msg(v, thr);
+            c2b[pos] = v;
+        }
+    }
+}
+
+template <int MODE, int DC>
+__global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const DeviceCode& c = a.code;
+    double* total = reinterpret_cast<double*>(smem);               // [n]
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + (size_t)c.n_pad * 8);  // [0]=frame, [2..3]=any flags
+    const int tid = threadIdx.x;
+    double* c2b = a.c2b + (size_t)blockIdx.x * a.c2b_stride;
+    const bool clamp_on = a.clamp_on != 0;
+    uint32_t any_k = 0;
+    if (tid == 0) { ctl[2] = 0; ctl[3] = 0; }
+
+    for (;;) {
+        if (tid == 0) ctl[0] = atomicAdd(a.counter, 1u);
+        __syncthreads();
+        const uint32_t f = ctl[0];
+        if (f >= a.n_frames) break;
+
+        // ---- prologue: syndrome bits of this thread's checks, channel LLRs
+        uint32_t synmask = 0;
+        {
+            int r = 0;
+            for (int j = tid; j < c.m; j += kDecodeBlock, ++r) {
+                int s;
+                if (MODE == kModeLlr) {
+                    s = a.syn[(size_t)f * c.m + j] != 0;
+                } else {
+                    // calculate_syndrome_irregular on Alice's key (:413-414)
+                    const uint64_t* aw = a.alice_w + (size_t)f * a.words;
+                    const int deg = c.chk_deg[j];
+                    s = 0;
+                    for (int k = 0; k < deg; ++k) {
+                        const int bit = c.chk_bits[k * c.m_pad + j];
+                        s ^= (int)((aw[bit >> 6] >> (bit & 63)) & 1u);
+                    }
+                }
+                synmask |= (uint32_t)s << r;
+            }
+        }
+        uint32_t bobmask = 0;
+        {
+            int r = 0;
+            for (int i = tid; i < c.n; i += kDecodeBlock, ++r) {
+                double l;
+                if (MODE == kModeLlr) {
+                    l = a.llr[(size_t)f * c.n + i];
+                } else {
+                    const uint64_t w = a.bob_w[(size_t)f * a.words + (i >> 6)];
+                    const uint32_t bb = (uint32_t)((w >> (i & 63)) & 1u);
+                    bobmask |= bb << r;
+                    l = bb ? -a.log_p : a.log_p;     // qkd_ldpc_algorithm.cpp:402-405
+                }
+                total[i] = l;
+            }
+        }
+        __syncthreads();
+
+        // ---- iterations (qkd_ldpc_algorithm.cpp:212-330)
+        bool done = false;
+        uint32_t it = 0;
+        for (; it < a.max_it; ++it) {
+            {
+                int r = 0;
+                for (int j = tid; j < c.m; j += kDecodeBlock, ++r)
+                    check_update<DC>(c, total, c2b, j, (synmask >> r) & 1u, it == 0, clamp_on, a.thr);
+            }
+            __syncthreads();
+            // bit phase: total_i = LLR_i + sum_k c2b(i,k), ascending checks (:256-267)
+            {
+                int r = 0;
+                for (int i = tid; i < c.n; i += kDecodeBlock, ++r) {
+                    double acc;
+                    if (MODE == kModeLlr) acc = a.llr[(size_t)f * c.n + i];
+                    else acc = ((bobmask >> r) & 1u) ? -a.log_p : a.log_p;
+                    const int deg = c.bit_deg[i];
+                    for (int k = 0; k < deg; ++k) acc = acc + c2b[c.bit_edge[k * c.n_pad + i]];
+                    total[i] = acc;
+                }
+            }
+            __syncthreads();
+            // syndrome of the hard decision (total <= 0 -> 1) vs target (:277-285)
+            bool mismatch = false;
+            {
+                int r = 0;
+                for (int j = tid; j < c.m; j += kDecodeBlock, ++r) {
+                    const int deg = c.chk_deg[j];
+                    int d = 0;
+                    for (int k = 0; k < deg; ++k) d ^= (total[c.chk_bits[k * c.m_pad + j]] <= 0.0);
+                    mismatch |= (d != (int)((synmask >> r) & 1u));
+                }
+            }
+            if (!block_any(mismatch, ctl + 2, any_k)) {
+                done = true;
+                break;
+            }
+        }
+
+        // ---- outputs: SP_result + last hard decision (+ keys_match)
+        bool key_mismatch = false;
+        for (int i = tid; i < c.n; i += kDecodeBlock) {
+            const uint8_t d = total[i] <= 0.0 ? 1 : 0;
+            if (a.bits_out) a.bits_out[(size_t)f * c.n + i] = d;
+            if (MODE == kModeKeys) {
+                const uint64_t w = a.alice_w[(size_t)f * a.words + (i >> 6)];
+                key_mismatch |= (uint8_t)((w >> (i & 63)) & 1u) != d;
+            }
+        }
+        if (MODE == kModeKeys) {
+            __syncthreads();
+            const bool km = block_any(key_mismatch, ctl + 2, any_k);
+            if (tid == 0 && a.key_ok) a.key_ok[f] = km ? 0 : 1;   // arrays_equal (:433)
+        }
+        if (tid == 0) {
+            a.iters[f] = done ? it + 1 : a.max_it;
+            a.sp_ok[f] = done ? 1 : 0;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- syndrome ---------------------------------------------------------------
+__global__ void syndrome_kernel(DeviceCode c, const uint8_t* bits, uint32_t n_frames, uint8_t* syn) {
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (size_t)n_frames * c.m) return;
+    const size_t f = gid / c.m;
+    const int j = (int)(gid - f * c.m);
+    const int deg = c.chk_deg[j];
+    int s = 0;
+    for (int k = 0; k < deg; ++k) s ^= bits[f * c.n + c.chk_bits[k * c.m_pad + j]] & 1;
+    syn[gid] = (uint8_t)s;
+}
+
+// ---- bit packing ------------------------------------------------------------
+__global__ void pack_kernel(const uint8_t* bytes, uint32_t n, uint32_t words, uint32_t n_frames,
+                            uint64_t* out) {
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (size_t)n_frames * words) return;
+    const size_t f = gid / words;
+    const uint32_t w = (uint32_t)(gid - f * words);
+    uint64_t v = 0;
+    const uint32_t lo = w * 64, hi = min(n, lo + 64);
+    for (uint32_t i = lo; i < hi; ++i) v |= (uint64_t)(bytes[f * n + i] & 1u) << (i - lo);
+    out[gid] = v;
+}
+
+__global__ void unpack_kernel(const uint64_t* words_in, uint32_t n, uint32_t words, uint32_t n_frames,
+                              uint8_t* out) {
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (size_t)n_frames * n) return;
+    const size_t f = gid / n;
+    const uint32_t i = (uint32_t)(gid - f * n);
+    out[gid] = (uint8_t)((words_in[f * words + (i >> 6)] >> (i & 63)) & 1u);
+}
+
+// ---- key generation: one thread per frame ------------------------------------
+// generate_random_bit_array + introduce_errors (array_and_matrix_operations.cpp:424-460)
+__global__ void keygen_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n_frames, uint32_t n,
+                              uint32_t words, uint32_t ne, uint64_t* alice_w, uint64_t* bob_w,
+                              uint32_t* low_scratch, double* exact_q) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n_frames) return;
+    qkdr::Xoshiro256pp g;
+    g.seed(seeds[f] + offset);
+    uint64_t* A = alice_w + (size_t)f * words;
+    uint64_t* B = bob_w + (size_t)f * words;
+    for (uint32_t w = 0; w < words; ++w) {
+        const uint32_t nb = min(64u, n - w * 64);
+        uint64_t v = 0;
+        for (uint32_t b = 0; b < nb; ++b) v |= (g.next() >> 63) << b;
+        A[w] = v;
+        B[w] = v;
+    }
+    uint32_t* low = low_scratch + (size_t)f * ne;
+    qkdr::shuffle_low_positions(g, n, ne, low);
+    for (uint32_t p = 0; p < ne; ++p) {
+        const uint32_t pos = low[p];
+        B[pos >> 6] ^= 1ull << (pos & 63);
+    }
+    if (exact_q) exact_q[f] = (double)ne / (double)n;
+}
+
+// ---- batch reduction (simulation.cpp:252-312) ----------------------------------
+__global__ void counters_kernel(const uint32_t* iters, const uint8_t* sp, const uint8_t* ko,
+                                uint32_t n_frames, qkd_counters* out) {
+    __shared__ unsigned long long s_sum[5];
+    __shared__ uint32_t s_min, s_max;
+    if (threadIdx.x < 5) s_sum[threadIdx.x] = 0;
+    if (threadIdx.x == 0) { s_min = 0xffffffffu; s_max = 0; }
+    __syncthreads();
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < n_frames) {
+        atomicAdd(&s_sum[0], 1ull);
+        if (sp[f]) {
+            const unsigned long long it = iters[f];
+            atomicAdd(&s_sum[1], 1ull);
+            if (!ko || ko[f]) atomicAdd(&s_sum[2], 1ull);
+            atomicAdd(&s_sum[3], it);
+            atomicAdd(&s_sum[4], it * it);
+            atomicMin(&s_min, (uint32_t)it);
+            atomicMax(&s_max, (uint32_t)it);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd((unsigned long long*)&out->frames, s_sum[0]);
+        atomicAdd((unsigned long long*)&out->sp_ok, s_sum[1]);
+        atomicAdd((unsigned long long*)&out->ldpc_ok, s_sum[2]);
+        atomicAdd((unsigned long long*)&out->sum_iters, s_sum[3]);
+        atomicAdd((unsigned long long*)&out->sum_iters_sq, s_sum[4]);
+        atomicMin(&out->min_iters, s_min);
+        atomicMax(&out->max_iters, s_max);
+    }
+}
+
+__global__ void counters_init_kernel(qkd_counters* c) {
+    c->frames = c->sp_ok = c->ldpc_ok = c->sum_iters = c->sum_iters_sq = 0;
+    c->min_iters = 0xffffffffu;
+    c->max_iters = 0;
+}
+
+// ---- launch plumbing --------------------------------------------------------
+
+using DecodeFn = void (*)(DecodeArgs);
+
+template <int MODE>
+static DecodeFn pick_decode(int max_dc) {
+    if (max_dc <= 6) return decode_kernel<MODE, 6>;
+    if (max_dc <= 8) return decode_kernel<MODE, 8>;
+    return decode_kernel<MODE, 16>;
+}
+
+static size_t decode_lds_bytes(const qkd_code* c) { return (size_t)c->n_pad * 8 + 16; }
+
+// Resident workgroups of decode_kernel for this code on its device.
+static qkd_status decode_grid(const qkd_code* c, DecodeFn fn, int* grid) {
+    const size_t lds = decode_lds_bytes(c);
+    QKD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int per_cu = 0;
+    QKD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, kDecodeBlock, lds));
+    if (per_cu < 1) return set_error(QKD_ERR_UNSUPPORTED, "decode kernel cannot be resident (LDS %zu B)", lds);
+    *grid = per_cu * c->cu_count;
+    return QKD_OK;
+}
+
+qkd_status ws_reserve_decode(qkd_workspace* ws, size_t slots) {
+    const qkd_code* c = ws->code;
+    if (!ws->counter) QKD_HIP(hipMalloc(&ws->counter, 64));
+    if (ws->c2b_slots >= slots) return QKD_OK;
+    if (ws->c2b) QKD_HIP(hipFree(ws->c2b));
+    ws->c2b = nullptr;
+    ws->c2b_slots = 0;
+    const size_t bytes = slots * (size_t)c->max_dc * c->m_pad * sizeof(double);
+    if (hipMalloc(&ws->c2b, bytes) != hipSuccess)
+        return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate %zu B of c2b scratch", bytes);
+    ws->c2b_slots = slots;
+    return QKD_OK;
+}
+
+qkd_status ws_reserve_keys(qkd_workspace* ws, size_t frames, size_t low_words) {
+    const qkd_code* c = ws->code;
+    const size_t words = (size_t)(c->n + 63) / 64;
+    if (ws->key_frames < frames) {
+        if (ws->alice_w) QKD_HIP(hipFree(ws->alice_w));
+        if (ws->bob_w) QKD_HIP(hipFree(ws->bob_w));
+        ws->alice_w = ws->bob_w = nullptr;
+        ws->key_frames = 0;
+        if (hipMalloc(&ws->alice_w, frames * words * 8) != hipSuccess ||
+            hipMalloc(&ws->bob_w, frames * words * 8) != hipSuccess)
+            return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate keys for %zu frames", frames);
+        ws->key_frames = frames;
+    }
+    if (ws->low_words < low_words) {
+        if (ws->low) QKD_HIP(hipFree(ws->low));
+        ws->low = nullptr;
+        ws->low_words = 0;
+        if (hipMalloc(&ws->low, low_words * 4) != hipSuccess)
+            return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate shuffle scratch");
+        ws->low_words = low_words;
+    }
+    return QKD_OK;
+}
+
+static qkd_status ws_free(qkd_workspace* ws) {
+    DeviceGuard g(ws->device);
+    if (ws->c2b) (void)hipFree(ws->c2b);
+    if (ws->counter) (void)hipFree(ws->counter);
+    if (ws->alice_w) (void)hipFree(ws->alice_w);
+    if (ws->bob_w) (void)hipFree(ws->bob_w);
+    if (ws->low) (void)hipFree(ws->low);
+    if (ws->done) (void)hipEventDestroy(ws->done);
+    return QKD_OK;
+}
+
+static std::mutex g_default_ws_mu;
+
+qkd_workspace* resolve_ws(const qkd_code* code, qkd_workspace* ws) {
+    if (ws) return ws;
+    std::lock_guard<std::mutex> lk(g_default_ws_mu);
+    if (!code->default_ws) {
+        qkd_status s;
+        const_cast<qkd_code*>(code)->default_ws = qkd_workspace_create(code, &s);
+    }
+    return code->default_ws;
+}
+
+// Serialise users of one workspace across streams: wait for the previous
+// user's completion event, record ours after our launches.
+struct WsSession {
+    qkd_workspace* ws;
+    hipStream_t stream;
+    std::unique_lock<std::mutex> lk;
+    WsSession(qkd_workspace* w, hipStream_t s) : ws(w), stream(s), lk(w->mu) {
+        if (ws->done) (void)hipStreamWaitEvent(stream, ws->done, 0);
+    }
+    ~WsSession() {
+        if (!ws->done) (void)hipEventCreateWithFlags(&ws->done, hipEventDisableTiming);
+        if (ws->done) (void)hipEventRecord(ws->done, stream);
+    }
+};
+
+static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs& a, int mode,
+                                hipStream_t stream) {
+    DecodeFn fn = mode == kModeLlr ? pick_decode<kModeLlr>(c->max_dc) : pick_decode<kModeKeys>(c->max_dc);
+    int grid = 0;
+    qkd_status s = decode_grid(c, fn, &grid);
+    if (s != QKD_OK) return s;
+    grid = (int)std::min<size_t>((size_t)grid, a.n_frames);
+    s = ws_reserve_decode(ws, (size_t)grid);
+    if (s != QKD_OK) return s;
+    a.code = c->view();
+    a.c2b = ws->c2b;
+    a.c2b_stride = (size_t)c->max_dc * c->m_pad;
+    a.counter = ws->counter;
+    QKD_HIP(hipMemsetAsync(ws->counter, 0, 4, stream));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kDecodeBlock), decode_lds_bytes(c), stream, a);
+    QKD_HIP(hipGetLastError());
+    return QKD_OK;
+}
+
+static qkd_status check_frames(size_t n_frames) {
+    if (n_frames == 0) return set_error(QKD_ERR_INVALID_ARG, "n_frames must be > 0");
+    if (n_frames > 0xffffffffull) return set_error(QKD_ERR_INVALID_ARG, "n_frames too large");
+    return QKD_OK;
+}
+
+static qkd_status check_decode_params(uint32_t max_it, double thr, uint32_t flags) {
+    if (max_it < 1) return set_error(QKD_ERR_INVALID_ARG, "max_iterations must be >= 1");
+    if (flags & ~QKD_FLAG_THRESHOLD) return set_error(QKD_ERR_INVALID_ARG, "unknown flags 0x%x", flags);
+    if ((flags & QKD_FLAG_THRESHOLD) && !(thr > 0.0))
+        return set_error(QKD_ERR_INVALID_ARG, "message threshold must be > 0");
+    return QKD_OK;
+}
+
+static unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace qkd
+
+using namespace qkd;
+
+extern "C" {
+
+qkd_workspace* qkd_workspace_create(const qkd_code* code, qkd_status* status) {
+    if (!code) {
+        if (status) *status = set_error(QKD_ERR_INVALID_ARG, "null code");
+        return nullptr;
+    }
+    qkd_workspace* ws = new (std::nothrow) qkd_workspace();
+    if (!ws) {
+        if (status) *status = set_error(QKD_ERR_OUT_OF_MEMORY, "out of host memory");
+        return nullptr;
+    }
+    ws->code = code;
+    ws->device = code->device;
+    if (status) *status = QKD_OK;
+    return ws;
+}
+
+void qkd_workspace_destroy(qkd_workspace* ws) {
+    if (!ws) return;
+    ws_free(ws);
+    delete ws;
+}
+
+qkd_status qkd_syndrome_batch(const qkd_code* c, const uint8_t* bits, size_t n_frames, uint8_t* syn,
+                              void* stream) {
+    clear_error();
+    if (!c || !bits || !syn) return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    qkd_status s = check_frames(n_frames);
+    if (s != QKD_OK) return s;
+    DeviceGuard g(c->device);
+    const size_t total = n_frames * (size_t)c->m;
+    hipLaunchKernelGGL(syndrome_kernel, dim3(blocks_for(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                       c->view(), bits, (uint32_t)n_frames, syn);
+    QKD_HIP(hipGetLastError());
+    return QKD_OK;
+}
+
+qkd_status qkd_decode_batch(const qkd_code* c, qkd_workspace* ws, const double* llr,
+                            const uint8_t* syndrome, size_t n_frames, uint32_t max_iterations,
+                            double msg_threshold, uint32_t flags, uint8_t* bits_out,
+                            uint32_t* iterations, uint8_t* syndromes_match, void* stream) {
+    clear_error();
+    if (!c || !llr || !syndrome || !iterations || !syndromes_match)
+        return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    qkd_status s = check_frames(n_frames);
+    if (s == QKD_OK) s = check_decode_params(max_iterations, msg_threshold, flags);
+    if (s != QKD_OK) return s;
+    DeviceGuard g(c->device);
+    ws = resolve_ws(c, ws);
+    if (!ws) return set_error(QKD_ERR_OUT_OF_MEMORY, "no workspace");
+    WsSession sess(ws, (hipStream_t)stream);
+    DecodeArgs a{};
+    a.n_frames = (uint32_t)n_frames;
+    a.max_it = max_iterations;
+    a.thr = msg_threshold;
+    a.clamp_on = (flags & QKD_FLAG_THRESHOLD) ? 1 : 0;
+    a.llr = llr;
+    a.syn = syndrome;
+    a.bits_out = bits_out;
+    a.iters = iterations;
+    a.sp_ok = syndromes_match;
+    return launch_decode(c, ws, a, kModeLlr, (hipStream_t)stream);
+}
+
+// Shared by qkd_qkd_ldpc_batch and qkd_trials_batch: keys already packed in ws.
+static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_frames, double q,
+                              uint32_t max_it, double thr, uint32_t flags, uint8_t* bits_out,
+                              uint32_t* iters, uint8_t* sp_ok, uint8_t* key_ok, hipStream_t stream) {
+    DecodeArgs a{};
+    a.n_frames = (uint32_t)n_frames;
+    a.max_it = max_it;
+    a.thr = thr;
+    a.clamp_on = (flags & QKD_FLAG_THRESHOLD) ? 1 : 0;
+    a.alice_w = ws->alice_w;
+    a.bob_w = ws->bob_w;
+    a.words = (uint32_t)((c->n + 63) / 64);
+    a.log_p = std::log((1. - q) / q);          // host glibc log, qkd_ldpc_algorithm.cpp:400
+    a.bits_out = bits_out;
+    a.iters = iters;
+    a.sp_ok = sp_ok;
+    a.key_ok = key_ok;
+    return launch_decode(c, ws, a, kModeKeys, stream);
+}
+
+qkd_status qkd_qkd_ldpc_batch(const qkd_code* c, qkd_workspace* ws, const uint8_t* alice,
+                              const uint8_t* bob, size_t n_frames, double qber, uint32_t max_iterations,
+                              double msg_threshold, uint32_t flags, uint8_t* bits_out,
+                              uint32_t* iterations, uint8_t* syndromes_match, uint8_t* keys_match,
+                              void* stream) {
+    clear_error();
+    if (!c || !alice || !bob || !iterations || !syndromes_match)
+        return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    qkd_status s = check_frames(n_frames);
+    if (s == QKD_OK) s = check_decode_params(max_iterations, msg_threshold, flags);
+    if (s != QKD_OK) return s;
+    if (!(qber > 0.0 && qber < 1.0)) return set_error(QKD_ERR_INVALID_ARG, "QBER must be in (0,1)");
+    DeviceGuard g(c->device);
+    ws = resolve_ws(c, ws);
+    if (!ws) return set_error(QKD_ERR_OUT_OF_MEMORY, "no workspace");
+    WsSession sess(ws, (hipStream_t)stream);
+    s = ws_reserve_keys(ws, n_frames, 1);
+    if (s != QKD_OK) return s;
+    const uint32_t words = (uint32_t)((c->n + 63) / 64);
+    const size_t nw = n_frames * words;
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw, 256)), dim3(256), 0, (hipStream_t)stream, alice,
+                       (uint32_t)c->n, words, (uint32_t)n_frames, ws->alice_w);
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw, 256)), dim3(256), 0, (hipStream_t)stream, bob,
+                       (uint32_t)c->n, words, (uint32_t)n_frames, ws->bob_w);
+    QKD_HIP(hipGetLastError());
+    return decode_keys(c, ws, n_frames, qber, max_iterations, msg_threshold, flags, bits_out, iterations,
+                       syndromes_match, keys_match, (hipStream_t)stream);
+}
+
+static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uint64_t* seeds,
+                                 uint64_t offset, size_t n_frames, double q_nom, double* exact_q,
+                                 hipStream_t stream) {
+    if (!(q_nom > 0.0 && q_nom <= 1.0)) return set_error(QKD_ERR_INVALID_ARG, "QBER must be in (0,1]");
+    const uint64_t ne = qkdr::num_errors((uint32_t)c->n, q_nom);
+    if (ne == 0)
+        return set_error(QKD_ERR_QBER_TOO_SMALL, "Key size '%d' is too small for QBER.", c->n);
+    qkd_status s = ws_reserve_keys(ws, n_frames, n_frames * ne);
+    if (s != QKD_OK) return s;
+    const uint32_t words = (uint32_t)((c->n + 63) / 64);
+    hipLaunchKernelGGL(keygen_kernel, dim3(blocks_for(n_frames, 64)), dim3(64), 0, stream, seeds, offset,
+                       (uint32_t)n_frames, (uint32_t)c->n, words, (uint32_t)ne, ws->alice_w, ws->bob_w,
+                       ws->low, exact_q);
+    QKD_HIP(hipGetLastError());
+    return QKD_OK;
+}
+
+qkd_status qkd_keygen_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t* seeds,
+                            uint64_t seed_offset, size_t n_frames, double q_nominal, uint8_t* alice,
+                            uint8_t* bob, double* exact_qber, void* stream) {
+    clear_error();
+    if (!c || !seeds || !alice || !bob) return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    qkd_status s = check_frames(n_frames);
+    if (s != QKD_OK) return s;
+    DeviceGuard g(c->device);
+    ws = resolve_ws(c, ws);
+    if (!ws) return set_error(QKD_ERR_OUT_OF_MEMORY, "no workspace");
+    WsSession sess(ws, (hipStream_t)stream);
+    s = keygen_into_ws(c, ws, seeds, seed_offset, n_frames, q_nominal, exact_qber, (hipStream_t)stream);
+    if (s != QKD_OK) return s;
+    const uint32_t words = (uint32_t)((c->n + 63) / 64);
+    const size_t nb = n_frames * (size_t)c->n;
+    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(nb, 256)), dim3(256), 0, (hipStream_t)stream,
+                       ws->alice_w, (uint32_t)c->n, words, (uint32_t)n_frames, alice);
+    hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(nb, 256)), dim3(256), 0, (hipStream_t)stream,
+                       ws->bob_w, (uint32_t)c->n, words, (uint32_t)n_frames, bob);
+    QKD_HIP(hipGetLastError());
+    return QKD_OK;
+}
+
+qkd_status qkd_counters_batch(const uint32_t* iterations, const uint8_t* syndromes_match,
+                              const uint8_t* keys_match, size_t n_frames, qkd_counters* counters,
+                              int device, void* stream) {
+    clear_error();
+    if (!iterations || !syndromes_match || !counters) return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    qkd_status s = check_frames(n_frames);
+    if (s != QKD_OK) return s;
+    DeviceGuard g(device);
+    hipLaunchKernelGGL(counters_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counters);
+    hipLaunchKernelGGL(counters_kernel, dim3(blocks_for(n_frames, 256)), dim3(256), 0, (hipStream_t)stream,
+                       iterations, syndromes_match, keys_match, (uint32_t)n_frames, counters);
+    QKD_HIP(hipGetLastError());
+    return QKD_OK;
+}
+
+qkd_status qkd_trials_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t* seeds,
+                            uint64_t seed_offset, size_t n_frames, double q_nominal,
+                            uint32_t max_iterations, double msg_threshold, uint32_t flags,
+                            uint32_t* iterations, uint8_t* syndromes_match, uint8_t* keys_match,
+                            double* exact_qber, qkd_counters* counters, void* stream) {
+    clear_error();
+    if (!c || !seeds || !iterations || !syndromes_match)
+        return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    qkd_status s = check_frames(n_frames);
+    if (s == QKD_OK) s = check_decode_params(max_iterations, msg_threshold, flags);
+    if (s != QKD_OK) return s;
+    DeviceGuard g(c->device);
+    ws = resolve_ws(c, ws);
+    if (!ws) return set_error(QKD_ERR_OUT_OF_MEMORY, "no workspace");
+    WsSession sess(ws, (hipStream_t)stream);
+    s = keygen_into_ws(c, ws, seeds, seed_offset, n_frames, q_nominal, exact_qber, (hipStream_t)stream);
+    if (s != QKD_OK) return s;
+    const double q = (double)qkdr::num_errors((uint32_t)c->n, q_nominal) / (double)c->n;
+    s = decode_keys(c, ws, n_frames, q, max_iterations, msg_threshold, flags, nullptr, iterations,
+                    syndromes_match, keys_match, (hipStream_t)stream);
+    if (s != QKD_OK) return s;
+    if (counters) {
+        hipLaunchKernelGGL(counters_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counters);
+        hipLaunchKernelGGL(counters_kernel, dim3(blocks_for(n_frames, 256)), dim3(256), 0,
+                           (hipStream_t)stream, iterations, syndromes_match, keys_match,
+                           (uint32_t)n_frames, counters);
+        QKD_HIP(hipGetLastError());
+    }
+    return QKD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,386 @@
+// host.cpp — code objects, matrix readers, errors and host helpers of the
+// C ABI (include/qkd_ldpc.h). Device kernels live in decode.hip.
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <new>
+#include <sstream>
+
+#include "qkd_internal.h"
+#include "qkd_rng.h"
+
+namespace qkd {
+
+static thread_local std::string g_last_error;
+
+qkd_status set_error(qkd_status s, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return s;
+}
+
+void clear_error() { g_last_error.clear(); }
+
+static int32_t round_up(int32_t x, int32_t a) { return (x + a - 1) / a * a; }
+
+static void free_device(qkd_code* c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    if (c->d_chk_bits) (void)hipFree(c->d_chk_bits);
+    if (c->d_chk_deg) (void)hipFree(c->d_chk_deg);
+    if (c->d_bit_edge) (void)hipFree(c->d_bit_edge);
+    if (c->d_bit_deg) (void)hipFree(c->d_bit_deg);
+    c->d_chk_bits = nullptr;
+    c->d_chk_deg = nullptr;
+    c->d_bit_edge = nullptr;
+    c->d_bit_deg = nullptr;
+}
+
+// Validate the check-side CSR, derive the bit side, upload the ELL layouts.
+static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* cptr,
+                             const int32_t* cidx, int device) {
+    if (n <= 0 || m <= 0 || !cptr || !cidx)
+        return set_error(QKD_ERR_INVALID_ARG, "qkd_code_create: n=%d m=%d, null adjacency", n, m);
+    if (cptr[0] != 0) return set_error(QKD_ERR_BAD_CODE, "check_ptr[0] must be 0");
+    for (int32_t j = 0; j < m; ++j)
+        if (cptr[j + 1] < cptr[j])
+            return set_error(QKD_ERR_BAD_CODE, "check_ptr not monotone at check %d", j);
+    const int32_t e = cptr[m];
+    if (e <= 0) return set_error(QKD_ERR_BAD_CODE, "code has no edges");
+    int32_t max_dc = 0;
+    std::vector<int32_t> bdeg(n, 0);
+    for (int32_t j = 0; j < m; ++j) {
+        const int32_t d = cptr[j + 1] - cptr[j];
+        max_dc = std::max(max_dc, d);
+        for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) {
+            const int32_t b = cidx[k];
+            if (b < 0 || b >= n)
+                return set_error(QKD_ERR_BAD_CODE, "check %d: bit index %d out of range [0,%d)", j, b, n);
+            if (k > cptr[j] && cidx[k - 1] >= b)
+                return set_error(cidx[k - 1] == b ? QKD_ERR_BAD_CODE : QKD_ERR_UNSORTED,
+                                 "check %d: bit list not strictly ascending at slot %d (%d after %d)",
+                                 j, k - cptr[j], b, cidx[k - 1]);
+            bdeg[b]++;
+        }
+    }
+    int32_t max_dv = 0;
+    for (int32_t i = 0; i < n; ++i) max_dv = std::max(max_dv, bdeg[i]);
+    if (max_dc > kMaxCheckDegree)
+        return set_error(QKD_ERR_UNSUPPORTED, "check degree %d exceeds %d", max_dc, kMaxCheckDegree);
+    if (max_dv > 255) return set_error(QKD_ERR_UNSUPPORTED, "bit degree %d exceeds 255", max_dv);
+    if (n > kMaxBitsLds)
+        return set_error(QKD_ERR_UNSUPPORTED, "N=%d exceeds the LDS-resident limit %d", n, kMaxBitsLds);
+
+    c->device = device;
+    c->n = n;
+    c->m = m;
+    c->e = e;
+    c->max_dc = max_dc;
+    c->max_dv = max_dv;
+    c->check_ptr.assign(cptr, cptr + m + 1);
+    c->check_idx.assign(cidx, cidx + e);
+    // bit side: iterate checks ascending -> each bit row ascending
+    c->bit_ptr.assign(n + 1, 0);
+    for (int32_t i = 0; i < n; ++i) c->bit_ptr[i + 1] = c->bit_ptr[i] + bdeg[i];
+    c->bit_idx.assign(e, 0);
+    std::vector<int32_t> fill(c->bit_ptr.begin(), c->bit_ptr.end() - 1);
+    c->n_pad = round_up(n, 64);
+    c->m_pad = round_up(m, 64);
+    std::vector<int32_t> chk_bits((size_t)max_dc * c->m_pad, -1);
+    std::vector<uint8_t> chk_deg(m, 0);
+    std::vector<int32_t> bit_edge((size_t)max_dv * c->n_pad, -1);
+    std::vector<uint8_t> bit_deg(n, 0);
+    for (int32_t j = 0; j < m; ++j) {
+        chk_deg[j] = (uint8_t)(cptr[j + 1] - cptr[j]);
+        for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) {
+            const int32_t slot = k - cptr[j];
+            const int32_t b = cidx[k];
+            chk_bits[(size_t)slot * c->m_pad + j] = b;
+            const int32_t bk = fill[b] - c->bit_ptr[b];
+            c->bit_idx[fill[b]++] = j;
+            bit_edge[(size_t)bk * c->n_pad + b] = slot * c->m_pad + j;
+        }
+    }
+    bool reg = true;
+    for (int32_t i = 0; i < n; ++i) {
+        bit_deg[i] = (uint8_t)bdeg[i];
+        reg = reg && bdeg[i] == bdeg[0];
+    }
+    for (int32_t j = 0; j < m; ++j) reg = reg && chk_deg[j] == chk_deg[0];
+    c->is_regular = reg ? 1 : 0;
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_error(QKD_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev)
+        return set_error(QKD_ERR_INVALID_ARG, "device %d out of range (%d devices)", device, ndev);
+    DeviceGuard g(device);
+    QKD_HIP(hipDeviceGetAttribute(&c->cu_count, hipDeviceAttributeMultiprocessorCount, device));
+    QKD_HIP(hipMalloc(&c->d_chk_bits, chk_bits.size() * sizeof(int32_t)));
+    QKD_HIP(hipMalloc(&c->d_chk_deg, chk_deg.size()));
+    QKD_HIP(hipMalloc(&c->d_bit_edge, bit_edge.size() * sizeof(int32_t)));
+    QKD_HIP(hipMalloc(&c->d_bit_deg, bit_deg.size()));
+    QKD_HIP(hipMemcpy(c->d_chk_bits, chk_bits.data(), chk_bits.size() * sizeof(int32_t),
+                      hipMemcpyHostToDevice));
+    QKD_HIP(hipMemcpy(c->d_chk_deg, chk_deg.data(), chk_deg.size(), hipMemcpyHostToDevice));
+    QKD_HIP(hipMemcpy(c->d_bit_edge, bit_edge.data(), bit_edge.size() * sizeof(int32_t),
+                      hipMemcpyHostToDevice));
+    QKD_HIP(hipMemcpy(c->d_bit_deg, bit_deg.data(), bit_deg.size(), hipMemcpyHostToDevice));
+    return QKD_OK;
+}
+
+static qkd_code* make_code(int32_t n, int32_t m, const int32_t* cptr, const int32_t* cidx,
+                           int device, qkd_status* status) {
+    qkd_code* c = new (std::nothrow) qkd_code();
+    qkd_status s = c ? build_code(c, n, m, cptr, cidx, device)
+                     : set_error(QKD_ERR_OUT_OF_MEMORY, "out of host memory");
+    if (s != QKD_OK) {
+        free_device(c);
+        delete c;
+        c = nullptr;
+    }
+    if (status) *status = s;
+    return c;
+}
+
+// ---- readers ---------------------------------------------------------------
+
+// istringstream >> int semantics: integers up to the first non-integer token.
+static void parse_ints(const std::string& line, std::vector<long>& out) {
+    out.clear();
+    const char* s = line.c_str();
+    for (;;) {
+        while (*s == ' ' || *s == '\t' || *s == '\r' || *s == '\v' || *s == '\f' || *s == '\n') s++;
+        if (!*s) break;
+        char* end = nullptr;
+        errno = 0;
+        long v = strtol(s, &end, 10);
+        if (end == s || errno == ERANGE || v > INT32_MAX || v < INT32_MIN) break;
+        out.push_back(v);
+        s = end;
+    }
+}
+
+static bool read_lines(const char* path, std::vector<std::vector<long>>& rows) {
+    std::ifstream f(path);
+    if (!f.is_open()) return false;
+    std::string line;
+    std::vector<long> v;
+    while (std::getline(f, line)) {
+        parse_ints(line, v);
+        rows.push_back(v);
+    }
+    return true;
+}
+
+// read_sparse_alist_matrix (reference array_and_matrix_operations.cpp:109-292)
+static qkd_status parse_alist(const char* path, int32_t& n, int32_t& m, std::vector<int32_t>& cptr,
+                              std::vector<int32_t>& cidx) {
+    std::vector<std::vector<long>> v;
+    if (!path || !read_lines(path, v))
+        return set_error(QKD_ERR_IO, "Failed to open file: %s", path ? path : "(null)");
+    if (v.empty()) return set_error(QKD_ERR_IO, "File is empty or cannot be read properly: %s", path);
+    if (v.size() < 4) return set_error(QKD_ERR_IO, "Insufficient data in the file: %s", path);
+    if (v[0].size() != 2 || v[1].size() != 2)
+        return set_error(QKD_ERR_IO, "File format does not match the alist format: %s", path);
+    const long cols = v[0][0], rows = v[0][1];
+    const size_t nb = v[2].size(), nc = v[3].size();
+    if (v.size() < 4 + nb + nc) return set_error(QKD_ERR_IO, "Insufficient data in the file: %s", path);
+    if (cols != (long)nb)
+        return set_error(QKD_ERR_IO, "Number of columns '%ld' is not the same as the length of the third line '%zu'. File: %s", cols, nb, path);
+    if (rows != (long)nc)
+        return set_error(QKD_ERR_IO, "Number of rows '%ld' is not the same as the length of the fourth line '%zu'. File: %s", rows, nc, path);
+    for (size_t i = 0; i < nb + nc; ++i) {
+        const auto& L = v[4 + i];
+        const long w = i < nb ? v[2][i] : v[3][i - nb];
+        long nz = 0;
+        for (long x : L) nz += (x != 0);
+        if (nz != w || w < 0 || (size_t)w > L.size())
+            return set_error(QKD_ERR_IO, "Number of non-zero elements '%ld' in the line '%zu' does not match the weight '%ld'. File: %s", nz, 5 + i, w, path);
+    }
+    n = (int32_t)cols;
+    m = (int32_t)rows;
+    // check_nodes rows (the first weight entries of each check line, 1-based)
+    cptr.assign(m + 1, 0);
+    cidx.clear();
+    for (int32_t j = 0; j < m; ++j) {
+        const auto& L = v[4 + nb + j];
+        for (long k = 0; k < v[3][j]; ++k) cidx.push_back((int32_t)(L[k] - 1));
+        cptr[j + 1] = (int32_t)cidx.size();
+    }
+    // bit_nodes rows must describe the same edge set (the reference reads
+    // both and would route messages inconsistently if they disagree)
+    std::vector<std::vector<int32_t>> from_checks(n);
+    for (int32_t j = 0; j < m; ++j)
+        for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) {
+            const int32_t b = cidx[k];
+            if (b < 0 || b >= n)
+                return set_error(QKD_ERR_BAD_CODE, "check %d lists bit %d outside [1,%d]. File: %s", j + 1, b + 1, n, path);
+            from_checks[b].push_back(j);
+        }
+    for (int32_t i = 0; i < n; ++i) {
+        const auto& L = v[4 + i];
+        std::vector<int32_t> row;
+        for (long k = 0; k < v[2][i]; ++k) row.push_back((int32_t)(L[k] - 1));
+        if (row != from_checks[i]) {
+            std::vector<int32_t> s = row;
+            std::sort(s.begin(), s.end());
+            if (s == from_checks[i])
+                return set_error(QKD_ERR_UNSORTED, "bit %d: check list not ascending. File: %s", i + 1, path);
+            return set_error(QKD_ERR_BAD_CODE, "bit %d: check list disagrees with the check rows. File: %s", i + 1, path);
+        }
+    }
+    return QKD_OK;
+}
+
+// read_dense_matrix (reference array_and_matrix_operations.cpp:295-421)
+static qkd_status parse_dense(const char* path, int32_t& n, int32_t& m, std::vector<int32_t>& cptr,
+                              std::vector<int32_t>& cidx) {
+    std::vector<std::vector<long>> v;
+    if (!path || !read_lines(path, v))
+        return set_error(QKD_ERR_IO, "Failed to open file: %s", path ? path : "(null)");
+    if (v.empty()) return set_error(QKD_ERR_IO, "File is empty or cannot be read properly: %s", path);
+    for (const auto& r : v)
+        for (long x : r)
+            if (x != 0 && x != 1)
+                return set_error(QKD_ERR_IO, "Parity check matrix can only take values 0 or 1. File: %s", path);
+    for (const auto& r : v)
+        if (r.size() != v[0].size())
+            return set_error(QKD_ERR_IO, "Different lengths of rows in a matrix. File: %s", path);
+    n = (int32_t)v[0].size();
+    m = (int32_t)v.size();
+    for (int32_t i = 0; i < n; ++i) {
+        long w = 0;
+        for (int32_t j = 0; j < m; ++j) w += v[j][i];
+        if (w <= 0)
+            return set_error(QKD_ERR_IO, "Column '%d' weight cannot be equal to or less than zero. File: %s", i + 1, path);
+    }
+    cptr.assign(m + 1, 0);
+    cidx.clear();
+    for (int32_t j = 0; j < m; ++j) {
+        for (int32_t i = 0; i < n; ++i)
+            if (v[j][i]) cidx.push_back(i);
+        if (cidx.size() == (size_t)cptr[j])
+            return set_error(QKD_ERR_IO, "Row '%d' weight cannot be equal to or less than zero. File: %s", j + 1, path);
+        cptr[j + 1] = (int32_t)cidx.size();
+    }
+    return QKD_OK;
+}
+
+}  // namespace qkd
+
+using namespace qkd;
+
+extern "C" {
+
+int qkd_abi_version(void) { return QKD_LDPC_ABI_VERSION; }
+
+const char* qkd_last_error(void) { return g_last_error.c_str(); }
+
+const char* qkd_status_string(qkd_status s) {
+    switch (s) {
+        case QKD_OK: return "ok";
+        case QKD_ERR_INVALID_ARG: return "invalid argument";
+        case QKD_ERR_BAD_CODE: return "malformed parity-check matrix";
+        case QKD_ERR_UNSORTED: return "adjacency row not ascending";
+        case QKD_ERR_QBER_TOO_SMALL: return "key size too small for QBER";
+        case QKD_ERR_DEVICE: return "HIP device error";
+        case QKD_ERR_OUT_OF_MEMORY: return "out of memory";
+        case QKD_ERR_IO: return "matrix file error";
+        case QKD_ERR_UNSUPPORTED: return "unsupported code shape";
+    }
+    return "unknown status";
+}
+
+int qkd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+qkd_code* qkd_code_create(int32_t n_bits, int32_t n_checks, const int32_t* check_ptr,
+                          const int32_t* check_idx, int device, qkd_status* status) {
+    clear_error();
+    return make_code(n_bits, n_checks, check_ptr, check_idx, device, status);
+}
+
+qkd_code* qkd_code_from_alist(const char* path, int device, qkd_status* status) {
+    clear_error();
+    int32_t n = 0, m = 0;
+    std::vector<int32_t> cptr, cidx;
+    qkd_status s = parse_alist(path, n, m, cptr, cidx);
+    if (s != QKD_OK) {
+        if (status) *status = s;
+        return nullptr;
+    }
+    return make_code(n, m, cptr.data(), cidx.data(), device, status);
+}
+
+qkd_code* qkd_code_from_dense(const char* path, int device, qkd_status* status) {
+    clear_error();
+    int32_t n = 0, m = 0;
+    std::vector<int32_t> cptr, cidx;
+    qkd_status s = parse_dense(path, n, m, cptr, cidx);
+    if (s != QKD_OK) {
+        if (status) *status = s;
+        return nullptr;
+    }
+    return make_code(n, m, cptr.data(), cidx.data(), device, status);
+}
+
+void qkd_code_destroy(qkd_code* code) {
+    if (!code) return;
+    if (code->default_ws) qkd_workspace_destroy(code->default_ws);
+    free_device(code);
+    delete code;
+}
+
+qkd_status qkd_code_get_info(const qkd_code* c, qkd_code_info* info) {
+    if (!c || !info) return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    info->n_bits = c->n;
+    info->n_checks = c->m;
+    info->n_edges = c->e;
+    info->max_bit_degree = c->max_dv;
+    info->max_check_degree = c->max_dc;
+    info->is_regular = c->is_regular;
+    info->device = c->device;
+    return QKD_OK;
+}
+
+qkd_status qkd_code_get_adjacency(const qkd_code* c, int32_t* check_ptr, int32_t* check_idx,
+                                  int32_t* bit_ptr, int32_t* bit_idx) {
+    if (!c) return set_error(QKD_ERR_INVALID_ARG, "null code");
+    if (check_ptr) std::memcpy(check_ptr, c->check_ptr.data(), c->check_ptr.size() * 4);
+    if (check_idx) std::memcpy(check_idx, c->check_idx.data(), c->check_idx.size() * 4);
+    if (bit_ptr) std::memcpy(bit_ptr, c->bit_ptr.data(), c->bit_ptr.size() * 4);
+    if (bit_idx) std::memcpy(bit_idx, c->bit_idx.data(), c->bit_idx.size() * 4);
+    return QKD_OK;
+}
+
+qkd_status qkd_make_seeds(uint64_t simulation_seed, size_t count, uint64_t* seeds) {
+    if (count && !seeds) return set_error(QKD_ERR_INVALID_ARG, "null seeds");
+    qkdr::Xoshiro256pp g;
+    g.seed(simulation_seed);
+    for (size_t i = 0; i < count; ++i) seeds[i] = g.next();
+    return QKD_OK;
+}
+
+qkd_status qkd_qber_range(double begin, double end, double step, double* values, size_t capacity,
+                          size_t* count) {
+    if (!count || !(step > 0.0)) return set_error(QKD_ERR_INVALID_ARG, "bad QBER range");
+    const double r = std::round((end - begin) / step);
+    const size_t steps = r > 0 ? (size_t)r : 0;
+    for (size_t j = 0; j < steps && j < capacity && values; ++j) values[j] = begin + (double)j * step;
+    *count = steps;
+    return QKD_OK;
+}
+
+}  // extern "C"

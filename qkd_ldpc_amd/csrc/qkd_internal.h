@@ -1,0 +1,108 @@
+// qkd_internal.h — shared definitions of the HIP library (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/qkd_ldpc.h"
+
+namespace qkd {
+
+// Threads per decode workgroup: one workgroup decodes one frame at a time.
+constexpr int kDecodeBlock = 1024;
+// Largest check degree the register-resident check update handles.
+constexpr int kMaxCheckDegree = 16;
+// The per-frame bit totals live in LDS as binary64: N <= this.
+constexpr int kMaxBitsLds = 20480;
+
+// Device-resident, immutable view of H.
+//   chk_bits[k * m_pad + j]  bit index of slot k of check j (ascending), -1 pad
+//   bit_edge[k * n_pad + i]  c2b storage slot (k' * m_pad + j) of the k-th
+//                            check of bit i (ascending), -1 pad
+// Slot-major ("ELL") layouts keep lane-consecutive checks / bits on
+// consecutive addresses.
+struct DeviceCode {
+    int32_t n, m, e;
+    int32_t n_pad, m_pad;
+    int32_t max_dv, max_dc;
+    const int32_t* chk_bits;
+    const uint8_t* chk_deg;
+    const int32_t* bit_edge;
+    const uint8_t* bit_deg;
+};
+
+}  // namespace qkd
+
+struct qkd_workspace {
+    const qkd_code* code = nullptr;
+    int device = 0;
+    std::mutex mu;
+    // decode scratch: one c2b region per resident workgroup
+    double* c2b = nullptr;
+    size_t c2b_slots = 0;
+    // dynamic frame queue counter (zeroed per launch)
+    uint32_t* counter = nullptr;
+    // packed alice / bob keys (uint64 words) for the fused paths
+    uint64_t* alice_w = nullptr;
+    uint64_t* bob_w = nullptr;
+    size_t key_frames = 0;
+    // keygen shuffle scratch (ne words per frame)
+    uint32_t* low = nullptr;
+    size_t low_words = 0;
+    hipEvent_t done = nullptr;
+};
+
+struct qkd_code {
+    int device = 0;
+    int32_t n = 0, m = 0, e = 0;
+    int32_t max_dv = 0, max_dc = 0, is_regular = 0;
+    int32_t n_pad = 0, m_pad = 0;
+    std::vector<int32_t> check_ptr, check_idx, bit_ptr, bit_idx;
+    int32_t* d_chk_bits = nullptr;
+    uint8_t* d_chk_deg = nullptr;
+    int32_t* d_bit_edge = nullptr;
+    uint8_t* d_bit_deg = nullptr;
+    int cu_count = 0;
+    qkd_workspace* default_ws = nullptr;
+
+    qkd::DeviceCode view() const {
+        return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc,
+                               d_chk_bits, d_chk_deg, d_bit_edge, d_bit_deg};
+    }
+};
+
+namespace qkd {
+
+qkd_status set_error(qkd_status s, const char* fmt, ...);
+void clear_error();
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+#define QKD_HIP(call)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return ::qkd::set_error(QKD_ERR_DEVICE, "%s failed: %s (%s:%d)", #call,       \
+                                    hipGetErrorString(e_), __FILE__, __LINE__);           \
+    } while (0)
+
+// Workspace helpers (decode.hip).
+qkd_status ws_reserve_decode(qkd_workspace* ws, size_t slots);
+qkd_status ws_reserve_keys(qkd_workspace* ws, size_t frames, size_t low_words);
+qkd_workspace* resolve_ws(const qkd_code* code, qkd_workspace* ws);
+
+}  // namespace qkd

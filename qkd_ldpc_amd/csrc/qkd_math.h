@@ -1,0 +1,266 @@
+// qkd_math.h — bit-exact binary64 tanh / atanh for the sum-product kernels.
+//
+// The reference decoder calls glibc 2.35 `tanh` and `atanh` once per edge per
+// half-iteration (reference src/qkd_ldpc_algorithm.cpp:224 and :241). Those are
+// the fdlibm algorithms layered on glibc's `__expm1` / `__log1p`, whose
+// polynomial tails glibc evaluates in a split (Estrin-like) order rather than
+// fdlibm's Horner chain. ROCm's ocml tanh/atanh round differently, so the
+// device cannot use them and still produce the reference's messages bit for
+// bit. This header restates those published algorithms once, as straight-line
+// binary64 code that compiles identically for the host (g++) and for gfx950
+// (hipcc). Both builds MUST use -ffp-contract=off: a fused a*b+c rounds once
+// and changes the last bit.
+//
+// Only round-to-nearest results matter here; floating-point exception flags
+// (inexact/underflow side effects in the C library) are not modelled.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define QKD_HD __host__ __device__ __forceinline__
+#else
+#define QKD_HD inline
+#endif
+
+namespace qkdm {
+
+QKD_HD uint64_t bits_of(double x) {
+    uint64_t u;
+    __builtin_memcpy(&u, &x, 8);
+    return u;
+}
+QKD_HD double from_bits(uint64_t u) {
+    double x;
+    __builtin_memcpy(&x, &u, 8);
+    return x;
+}
+QKD_HD int32_t hi32(double x) { return (int32_t)(bits_of(x) >> 32); }
+QKD_HD uint32_t lo32(double x) { return (uint32_t)bits_of(x); }
+// Replace the high 32 bits of x, keeping its low word.
+QKD_HD double set_hi32(double x, uint32_t hi) {
+    return from_bits(((uint64_t)hi << 32) | (bits_of(x) & 0xffffffffull));
+}
+
+// ---------------------------------------------------------------------------
+// expm1(x) = e^x - 1.  fdlibm s_expm1.c argument reduction and reconstruction;
+// the rational tail r1 is summed as (R1 + h2*R2) + h4*R3 (glibc dbl-64 order).
+// ---------------------------------------------------------------------------
+QKD_HD double expm1_ref(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;   // 0x3fe62e42 fee00000
+    const double ln2_lo = 1.90821492927058770002e-10;   // 0x3dea39ef 35793c76
+    const double invln2 = 1.44269504088896338700e+00;   // 0x3ff71547 652b82fe
+    const double o_threshold = 7.09782712893383973096e+02;
+    const double Q1 = -3.33333333333331316428e-02;
+    const double Q2 = 1.58730158725481460165e-03;
+    const double Q3 = -7.93650757867487942473e-05;
+    const double Q4 = 4.00821782732936239552e-06;
+    const double Q5 = -2.01099218183624371326e-07;
+
+    const uint32_t hword = (uint32_t)hi32(x);
+    const bool neg = (hword & 0x80000000u) != 0;
+    const uint32_t ahx = hword & 0x7fffffffu;
+
+    if (ahx >= 0x4043687Au) {                 // |x| >= 56 ln2
+        if (ahx >= 0x40862E42u) {             // |x| >= 709.78
+            if (ahx >= 0x7ff00000u) {
+                if (((ahx & 0xfffffu) | lo32(x)) != 0) return x + x;   // NaN
+                return neg ? -1.0 : x;                                 // +-inf
+            }
+            if (x > o_threshold) return 1.0e300 * 1.0e300;             // +inf
+        }
+        if (neg) return 1.0e-300 - 1.0;       // rounds to -1
+    }
+
+    double hi, lo, c = 0.0;
+    int k;
+    if (ahx > 0x3fd62e42u) {                  // |x| > ln2/2
+        if (ahx < 0x3FF0A2B2u) {              // |x| < 1.5 ln2
+            if (!neg) { hi = x - ln2_hi; lo = ln2_lo;  k = 1; }
+            else      { hi = x + ln2_hi; lo = -ln2_lo; k = -1; }
+        } else {
+            k = (int)(invln2 * x + (neg ? -0.5 : 0.5));
+            const double t = (double)k;
+            hi = x - t * ln2_hi;              // exact
+            lo = t * ln2_lo;
+        }
+        x = hi - lo;
+        c = (hi - x) - lo;
+    } else if (ahx < 0x3c900000u) {           // |x| < 2^-54
+        return x;
+    } else {
+        k = 0;
+    }
+
+    const double hfx = 0.5 * x;
+    const double hxs = x * hfx;
+    const double R1 = 1.0 + hxs * Q1;
+    const double h2 = hxs * hxs;
+    const double R2 = Q2 + hxs * Q3;
+    const double h4 = h2 * h2;
+    const double R3 = Q4 + hxs * Q5;
+    const double r1 = R1 + h2 * R2 + h4 * R3;
+    double t = 3.0 - r1 * hfx;
+    double e = hxs * ((r1 - t) / (6.0 - x * t));
+    if (k == 0) return x - (x * e - hxs);
+
+    e = (x * (e - c) - c);
+    e -= hxs;
+    if (k == -1) return 0.5 * (x - e) - 0.5;
+    if (k == 1) {
+        if (x < -0.25) return -2.0 * (e - (x + 0.5));
+        return 1.0 + 2.0 * (x - e);
+    }
+    double y;
+    if (k <= -2 || k > 56) {                  // exp(x)-1 ~ exp(x)
+        y = 1.0 - (e - x);
+        if (k == 1024) {
+            y = y * 2.0 * 0x1p1023;
+        } else {
+            y = set_hi32(y, (uint32_t)hi32(y) + ((uint32_t)k << 20));
+        }
+        return y - 1.0;
+    }
+    if (k < 20) {
+        t = from_bits((uint64_t)(0x3ff00000u - (0x200000u >> k)) << 32);   // 1 - 2^-k
+        y = t - (e - x);
+    } else {
+        t = from_bits((uint64_t)((uint32_t)(0x3ff - k) << 20) << 32);        // 2^-k
+        y = x - (e + t);
+        y += 1.0;
+    }
+    return set_hi32(y, (uint32_t)hi32(y) + ((uint32_t)k << 20));
+}
+
+// ---------------------------------------------------------------------------
+// log1p(x) = ln(1 + x).  fdlibm s_log1p.c reduction; the Lp tail is summed as
+// ((R1 + z2*R2) + z4*R3) + z6*R4 (glibc dbl-64 order).
+// ---------------------------------------------------------------------------
+QKD_HD double log1p_ref(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double two54 = 1.80143985094819840000e+16;
+    const double Lp1 = 6.666666666666735130e-01;
+    const double Lp2 = 3.999999999940941908e-01;
+    const double Lp3 = 2.857142874366239149e-01;
+    const double Lp4 = 2.222219843214978396e-01;
+    const double Lp5 = 1.818357216161805012e-01;
+    const double Lp6 = 1.531383769920937332e-01;
+    const double Lp7 = 1.479819860511658591e-01;
+
+    const int32_t hx = hi32(x);
+    const int32_t ax = hx & 0x7fffffff;
+    int32_t k = 1, hu = 0;
+    double f = 0.0, c = 0.0;
+
+    if (hx < 0x3FDA827A) {                    // x < 0.41422
+        if (ax >= 0x3ff00000) {               // x <= -1
+            if (x == -1.0) return -two54 / 0.0;   // -inf
+            return (x - x) / (x - x);             // NaN
+        }
+        if (ax < 0x3e200000) {                // |x| < 2^-29
+            if (ax < 0x3c900000) return x;
+            return x - x * x * 0.5;
+        }
+        if (hx > 0 || hx <= (int32_t)0xbfd2bec4) {   // -0.2929 < x < 0.41422
+            k = 0; f = x; hu = 1;
+        }
+    } else if (hx >= 0x7ff00000) {
+        return x + x;
+    }
+    if (k != 0) {
+        double u;
+        if (hx < 0x43400000) {
+            u = 1.0 + x;
+            hu = hi32(u);
+            k = (hu >> 20) - 1023;
+            c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);
+            c /= u;
+        } else {
+            u = x;
+            hu = hi32(u);
+            k = (hu >> 20) - 1023;
+            c = 0.0;
+        }
+        hu &= 0x000fffff;
+        if (hu < 0x6a09e) {
+            u = set_hi32(u, (uint32_t)hu | 0x3ff00000u);   // u in [1, sqrt2)
+        } else {
+            k += 1;
+            u = set_hi32(u, (uint32_t)hu | 0x3fe00000u);   // u/2
+            hu = (0x00100000 - hu) >> 2;
+        }
+        f = u - 1.0;
+    }
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)k;
+    if (hu == 0) {                            // |f| < 2^-20
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            c += dk * ln2_lo;
+            return dk * ln2_hi + c;
+        }
+        const double R = hfsq * (1.0 - 0.66666666666666666 * f);
+        if (k == 0) return f - R;
+        return dk * ln2_hi - ((R - (dk * ln2_lo + c)) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double R1 = z * Lp1;
+    const double z2 = z * z;
+    const double R2 = Lp2 + z * Lp3;
+    const double z4 = z2 * z2;
+    const double R3 = Lp4 + z * Lp5;
+    const double z6 = z4 * z2;
+    const double R4 = Lp6 + z * Lp7;
+    const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+}
+
+// ---------------------------------------------------------------------------
+// tanh — fdlibm s_tanh.c on expm1_ref.
+// ---------------------------------------------------------------------------
+QKD_HD double tanh_ref(double x) {
+    const int32_t jx = hi32(x);
+    const int32_t ix = jx & 0x7fffffff;
+    if (ix >= 0x7ff00000) {                   // inf or NaN
+        return (jx >= 0) ? 1.0 / x + 1.0 : 1.0 / x - 1.0;
+    }
+    double z;
+    if (ix < 0x40360000) {                    // |x| < 22
+        if ((ix | (int32_t)lo32(x)) == 0) return x;      // +-0
+        if (ix < 0x3c800000) return x * (1.0 + x);       // |x| < 2^-55
+        const double ax = __builtin_fabs(x);
+        if (ix >= 0x3ff00000) {               // |x| >= 1
+            const double t = expm1_ref(2.0 * ax);
+            z = 1.0 - 2.0 / (t + 2.0);
+        } else {
+            const double t = expm1_ref(-2.0 * ax);
+            z = -t / (t + 2.0);
+        }
+    } else {
+        z = 1.0;                              // 1 - tiny rounds to 1
+    }
+    return (jx >= 0) ? z : -z;
+}
+
+// ---------------------------------------------------------------------------
+// atanh — glibc dbl-64 e_atanh.c structure on log1p_ref.
+// ---------------------------------------------------------------------------
+QKD_HD double atanh_ref(double x) {
+    const double xa = __builtin_fabs(x);
+    double t;
+    if (xa < 0.5) {
+        if (xa < 0x1.0p-28) return x;
+        t = xa + xa;
+        t = 0.5 * log1p_ref(t + t * xa / (1.0 - xa));
+    } else if (xa < 1.0) {
+        t = 0.5 * log1p_ref((xa + xa) / (1.0 - xa));
+    } else {
+        if (xa > 1.0) return (x - x) / (x - x);          // |x| > 1: NaN
+        return x / 0.0;                                   // +-1: +-inf; NaN: NaN
+    }
+    return __builtin_copysign(t, x);
+}
+
+}  // namespace qkdm

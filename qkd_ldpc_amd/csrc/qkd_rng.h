@@ -1,0 +1,129 @@
+// qkd_rng.h — key-pair generation for one QKD trial, host and device.
+//
+// Reproduces the reference's per-trial key pair bit for bit:
+//   run_trial (reference src/simulation.cpp:161-168):
+//     Xoshiro256PlusPlus prng(seed);                         (XoshiroCpp 1.1)
+//     generate_random_bit_array(prng, N, alice);             (array_and_matrix_operations.cpp:424-431)
+//     q = introduce_errors(prng, alice, N, q_nom, bob);      (array_and_matrix_operations.cpp:434-460)
+//
+// Third-party algorithms restated (published, absent from the reference tree):
+//   * SplitMix64 seeding + xoshiro256++ (XoshiroCpp 1.1).
+//   * libstdc++ 11 uniform_int_distribution for a 64-bit engine: Lemire's
+//     multiply-shift with rejection (_S_nd, 128-bit product). For {0,1} it is
+//     exactly `draw >> 63` (threshold 0, never rejects).
+//   * libstdc++ 11 std::shuffle: for an even length, one lone swap of
+//     position 1 with {0,1}; then pairs (i, i+1) from one draw x in
+//     [0, (i+1)(i+2)): swap(i, x / (i+2)), swap(i+1, x % (i+2)).
+//
+// The reference materialises and shuffles a size_t[N] position array and then
+// flips bob[pos[p]] for p < ne = floor(N*q). Only pos[0..ne) matters, and this
+// forward shuffle never moves an element INTO a low position except as
+// "pos[x] = i" (the step index i). So the whole shuffle reduces to:
+//   steps i < ne:  low[i] = low[x]; low[x] = i      (exact simulation, ne slots)
+//   steps i >= ne: if (x < ne) low[x] = i            (last writer wins)
+// which needs ne words of scratch instead of N, with identical results.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define QKD_RHD __host__ __device__ __forceinline__
+#else
+#define QKD_RHD inline
+#endif
+
+namespace qkdr {
+
+struct Xoshiro256pp {
+    uint64_t s0, s1, s2, s3;
+
+    QKD_RHD static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+    QKD_RHD void seed(uint64_t seed) {
+        uint64_t z = seed;
+        uint64_t w[4];
+        for (int i = 0; i < 4; ++i) {
+            z += 0x9e3779b97f4a7c15ull;
+            uint64_t v = z;
+            v = (v ^ (v >> 30)) * 0xbf58476d1ce4e5b9ull;
+            v = (v ^ (v >> 27)) * 0x94d049bb133111ebull;
+            w[i] = v ^ (v >> 31);
+        }
+        s0 = w[0]; s1 = w[1]; s2 = w[2]; s3 = w[3];
+    }
+
+    QKD_RHD uint64_t next() {
+        const uint64_t r = rotl(s0 + s3, 23) + s0;
+        const uint64_t t = s1 << 17;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl(s3, 45);
+        return r;
+    }
+};
+
+QKD_RHD uint64_t mul_hi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+// uniform_int_distribution<size_t>{0, range-1}(g) with a full-range 64-bit g.
+QKD_RHD uint64_t lemire(Xoshiro256pp& g, uint64_t range) {
+    uint64_t d = g.next();
+    uint64_t low = d * range;
+    if (low < range) {
+        const uint64_t thr = (0 - range) % range;
+        while (low < thr) {
+            d = g.next();
+            low = d * range;
+        }
+    }
+    return mul_hi64(d, range);
+}
+
+// floor(N * q) as the reference computes it: static_cast<size_t>(N * q).
+QKD_RHD uint64_t num_errors(uint32_t n, double q) {
+    const double v = (double)n * q;
+    return v <= 0.0 ? 0 : (uint64_t)v;
+}
+
+// Shuffle-and-track: fills low[0..ne) with the positions that the reference's
+// shuffled array holds at indices [0, ne). `low` is caller scratch of ne words.
+// Consumes draws from g exactly as std::shuffle does.
+template <typename LowT>
+QKD_RHD void shuffle_low_positions(Xoshiro256pp& g, uint32_t n, uint32_t ne, LowT* low) {
+    for (uint32_t p = 0; p < ne; ++p) low[p] = p;
+    if (n <= 1) return;
+    uint32_t i = 1;
+    auto step = [&](uint32_t step_i, uint32_t x) {
+        if (step_i < ne) {
+            LowT v = low[x];          // x <= step_i < ne
+            low[x] = step_i;
+            low[step_i] = v;
+        } else if (x < ne) {
+            low[x] = step_i;
+        }
+    };
+    if ((n & 1u) == 0) {                              // even length: lone first swap
+        const uint32_t x = (uint32_t)(g.next() >> 63);  // uniform {0,1}
+        step(1, x);
+        i = 2;
+    }
+    while (i < n) {
+        const uint64_t b1 = (uint64_t)i + 2;
+        const uint64_t x = lemire(g, ((uint64_t)i + 1) * b1);
+        // x < (i+1)(i+2) < 2^64; both quotient and remainder fit 32 bits for n < 2^31.
+        const uint32_t a = (uint32_t)(x / b1);
+        const uint32_t b = (uint32_t)(x - (uint64_t)a * b1);
+        step(i, a);
+        step(i + 1, b);
+        i += 2;
+    }
+}
+
+}  // namespace qkdr

@@ -1,0 +1,254 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle, bit for bit.
+
+Every comparison is exact: decoded bits, iteration counts, syndrome match, key
+match, exact QBER and key pairs are integer/byte results of an fp64 algorithm
+whose transcendentals are restated bit-exactly (qkd_ldpc_amd/csrc/qkd_math.h).
+The oracle is the checker only (oracle/oracle.c, pinned in tests/test_oracle.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def Q():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import qkd_ldpc_amd as Q
+    return Q
+
+
+@pytest.fixture(scope="module")
+def H(Q, golden_code):
+    return Q.HMatrix.from_check_lists(int(golden_code["dims"][0]), golden_code["chk_off"],
+                                      golden_code["chk_idx"])
+
+
+def dev(x, dtype):
+    return torch.from_numpy(np.ascontiguousarray(x).astype(dtype)).cuda()
+
+
+def seeds_dev(seeds):
+    return torch.from_numpy(np.ascontiguousarray(seeds, np.uint64).view(np.int64)).cuda()
+
+
+def llr_of(bob, q):
+    lp = np.log((1 - q) / q)
+    return np.where(np.asarray(bob) == 1, -lp, lp)
+
+
+def decode_both(Q, H, ocode, llr, syn, max_it=50, thr=100.0, thr_on=True):
+    llr = np.atleast_2d(llr)
+    syn = np.atleast_2d(syn)
+    r = Q.sum_product_decoding(H, dev(llr, np.float64), dev(syn, np.uint8), max_it, thr, thr_on)
+    torch.cuda.synchronize()
+    bits = r.bits.cpu().numpy()
+    its = r.iterations.cpu().numpy()
+    ok = r.syndromes_match.cpu().numpy()
+    for f in range(llr.shape[0]):
+        want = ocode.decode(llr[f], syn[f], max_it, thr, thr_on)
+        assert its[f] == want["iters"], (f, its[f], want["iters"])
+        assert bool(ok[f]) == want["sp_ok"], f
+        assert (bits[f] == want["out"]).all(), f
+    return its, ok
+
+
+# ---- textbook known answers (BASELINE config 1) ------------------------------------
+
+@pytest.mark.parametrize("case", ["textbook_n6", "textbook_n10"])
+def test_textbook_cases(Q, probe, oracle_mod, case):
+    p = probe[case]
+    dense = np.array(p["dense"], np.uint8)
+    H = Q.HMatrix.from_dense_array(dense)
+    oc = oracle_mod.Code.from_dense(dense)
+    assert H.is_regular == bool(oc.is_regular)
+    alice = np.array(p["alice"])
+    bob = np.array(p["bob"])
+    syn = oc.syndrome(alice)
+    its, ok = decode_both(Q, H, oc, llr_of(bob, p["qber"]), syn, p["max_it"], p["thr"], True)
+    assert its[0] == p["iterations"] and bool(ok[0]) == p["syndromes_match"]
+    r = Q.qkd_ldpc(H, dev(alice[None], np.uint8), dev(bob[None], np.uint8), p["qber"], p["max_it"],
+                   p["thr"], True, want_bits=True)
+    torch.cuda.synchronize()
+    assert int(r.iterations[0]) == p["iterations"]
+    assert bool(r.keys_match[0]) == p["keys_match"]
+    assert (r.bits.cpu().numpy()[0] == alice).all()
+
+
+def test_all_dense_matrices_decode(Q, dense_codes, oracle_mod):
+    rng = np.random.default_rng(5)
+    for name, dense in dense_codes.items():
+        H = Q.HMatrix.from_dense_array(dense)
+        oc = oracle_mod.Code.from_dense(dense)
+        n = dense.shape[1]
+        alice = rng.integers(0, 2, (32, n))
+        bob = alice ^ (rng.random((32, n)) < 0.15)
+        syn = np.stack([oc.syndrome(a) for a in alice])
+        decode_both(Q, H, oc, llr_of(bob, 0.15), syn, 20, 100.0, True)
+
+
+# ---- N=10240 code, LLR entry point ------------------------------------------------
+
+@pytest.mark.parametrize("q_nom,frames", [(0.02, 24), (0.08, 12)])
+def test_decode_llr_matches_oracle(Q, H, oracle_code, oracle_mod, q_nom, frames):
+    seeds = oracle_mod.seeds(777, frames)
+    llr, syn = [], []
+    for s in seeds:
+        a, b, q = oracle_mod.keygen(int(s), 10240, q_nom)
+        llr.append(llr_of(b, q))
+        syn.append(oracle_code.syndrome(a))
+    decode_both(Q, H, oracle_code, np.stack(llr), np.stack(syn), 50, 100.0, True)
+
+
+@pytest.mark.parametrize("thr,thr_on,max_it", [(100.0, False, 50), (2.5, True, 50), (100.0, True, 1),
+                                               (100.0, True, 3), (0.5, True, 7)])
+def test_decode_threshold_and_iteration_caps(Q, H, oracle_code, oracle_mod, thr, thr_on, max_it):
+    seeds = oracle_mod.seeds(4242, 6)
+    llr, syn = [], []
+    for s in seeds:
+        a, b, q = oracle_mod.keygen(int(s), 10240, 0.05)
+        llr.append(llr_of(b, q))
+        syn.append(oracle_code.syndrome(a))
+    decode_both(Q, H, oracle_code, np.stack(llr), np.stack(syn), max_it, thr, thr_on)
+
+
+def test_decode_nan_and_inf_paths(Q, H, oracle_code):
+    """Zero LLRs give tanh(0)=0 -> 0/0 = NaN messages; huge LLRs give atanh(+-1) = +-inf.
+    The clamp lets NaN through (compare-based) and decisions send NaN to 0."""
+    rng = np.random.default_rng(11)
+    n, m = 10240, 5231
+    llr = rng.normal(2.0, 2.0, (6, n))
+    llr[0, rng.integers(0, n, 300)] = 0.0
+    llr[1, :] = 0.0
+    llr[2, rng.integers(0, n, 500)] = 900.0
+    llr[3, rng.integers(0, n, 500)] = -900.0
+    llr[4] = np.where(rng.random(n) < 0.5, 1e308, -1e308)
+    syn = rng.integers(0, 2, (6, m))
+    decode_both(Q, H, oracle_code, llr, syn, 8, 100.0, False)
+    decode_both(Q, H, oracle_code, llr, syn, 8, 100.0, True)
+
+
+def test_syndrome_batch(Q, H, oracle_code):
+    rng = np.random.default_rng(3)
+    bits = rng.integers(0, 2, (9, 10240))
+    got = Q.calculate_syndrome(H, dev(bits, np.uint8)).cpu().numpy()
+    for f in range(bits.shape[0]):
+        assert (got[f] == oracle_code.syndrome(bits[f])).all()
+
+
+# ---- key generation (run_trial's keys) -----------------------------------------------
+
+def test_keygen_matches_golden(Q, H, golden_vectors):
+    seeds = golden_vectors["kg_seeds"]
+    qn = golden_vectors["kg_qnom"]
+    k = len(seeds)
+    for g in range(len(qn) // k):
+        a, b, q = Q.keygen(H, seeds_dev(seeds), float(qn[g * k]))
+        torch.cuda.synchronize()
+        a = np.packbits(a.cpu().numpy(), axis=1)
+        b = np.packbits(b.cpu().numpy(), axis=1)
+        assert (a == golden_vectors["kg_alice"][g * k:(g + 1) * k]).all()
+        assert (b == golden_vectors["kg_bob"][g * k:(g + 1) * k]).all()
+        assert (q.cpu().numpy() == golden_vectors["kg_q"][g * k:(g + 1) * k]).all()
+
+
+def test_keygen_odd_and_tiny_lengths(Q, oracle_mod):
+    """Odd N skips std::shuffle's lone first swap; tiny N exercises ne close to N."""
+    rng = np.random.default_rng(9)
+    for n, q in [(7, 0.3), (6, 0.5), (9, 1.0), (101, 0.1), (1000, 0.02)]:
+        dense = np.zeros((n - 1, n), np.uint8)          # chain code: check j = bits (j, j+1)
+        for j in range(n - 1):
+            dense[j, j] = dense[j, j + 1] = 1
+        H = Q.HMatrix.from_dense_array(dense)
+        seeds = rng.integers(0, 2**63, 8, dtype=np.int64).astype(np.uint64)
+        a, b, qq = Q.keygen(H, seeds_dev(seeds), q)
+        torch.cuda.synchronize()
+        for f, s in enumerate(seeds):
+            wa, wb, wq = oracle_mod.keygen(int(s), n, q)
+            assert (a.cpu().numpy()[f] == wa).all() and (b.cpu().numpy()[f] == wb).all()
+            assert qq.cpu().numpy()[f] == wq
+
+
+def test_qber_too_small_raises(Q, H):
+    seeds = seeds_dev(np.arange(4, dtype=np.uint64))
+    with pytest.raises(Q.QkdError) as ei:
+        Q.run_trials(H, seeds, 1e-5)
+    assert "too small" in str(ei.value)
+
+
+# ---- fused trials: BASELINE configs 2 and 3 per frame ----------------------------------
+
+def test_trials_config2_full_batch(Q, H, probe, golden_vectors):
+    seeds = Q.make_seeds(777, 4096)
+    r = Q.run_trials(H, seeds_dev(seeds), 0.02, 0, 50, 100.0, True)
+    torch.cuda.synchronize()
+    assert (r.iterations.cpu().numpy() == golden_vectors["c2_iters"]).all()
+    assert (r.syndromes_match.cpu().numpy().astype(bool) == golden_vectors["c2_sp"]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c2_ko"]).all()
+    q = r.exact_qber.cpu().numpy()
+    assert (q == golden_vectors["c2_q"][0]).all()
+    st = Q.counters_to_stats(Q.read_counters(r.counters), 4096, 50, float(q[0]))
+    p = probe["config2"]
+    assert st["sum_iters_sp"] == p["sum_iterations"]
+    assert float(f"{st['iterations_successful_sp_mean']:.6g}") == p["mean_6sig"]
+    assert float(f"{st['iterations_successful_sp_std_dev']:.6g}") == p["std_6sig"]
+    assert st["iterations_successful_sp_min"] == p["min"]
+    assert st["iterations_successful_sp_max"] == p["max"]
+    assert st["fer"] == p["fer"]
+
+
+def test_trials_config3_every_point(Q, H, probe, golden_vectors):
+    seeds = seeds_dev(Q.make_seeds(777, 10000))
+    grid = golden_vectors["c3_qnom"]
+    for s, qn in enumerate(grid):
+        r = Q.run_trials(H, seeds, float(qn), s, 50, 100.0, True)
+        torch.cuda.synchronize()
+        assert (r.iterations.cpu().numpy() == golden_vectors["c3_iters"][s]).all(), s
+        assert (r.syndromes_match.cpu().numpy().astype(bool) == golden_vectors["c3_sp"][s]).all()
+        assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c3_ko"][s]).all()
+        st = Q.counters_to_stats(Q.read_counters(r.counters), 10000, 50,
+                                 float(r.exact_qber[0]))
+        pp = probe["config3"]["points"][s]
+        assert abs(st["fer"] - pp["fer"]) < 1e-12
+        assert abs(st["iterations_successful_sp_mean"] - pp["mean_it"]) <= 5e-4 + 1e-9
+
+
+def test_qkd_ldpc_batch_matches_trials(Q, H, golden_vectors):
+    """keygen -> qkd_ldpc (byte keys) equals the fused trial path."""
+    seeds = seeds_dev(Q.make_seeds(777, 512))
+    a, b, q = Q.keygen(H, seeds, 0.02)
+    r = Q.qkd_ldpc(H, a, b, float(q[0]), 50, 100.0, True, want_bits=True)
+    torch.cuda.synchronize()
+    assert (r.iterations.cpu().numpy() == golden_vectors["c2_iters"][:512]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c2_ko"][:512]).all()
+    ok = r.keys_match.cpu().numpy().astype(bool)
+    assert (r.bits.cpu().numpy()[ok] == a.cpu().numpy()[ok]).all()
+
+
+def test_workspace_and_streams(Q, H, golden_vectors):
+    """Two workspaces on two streams give the same per-frame results."""
+    seeds = seeds_dev(Q.make_seeds(777, 1024))
+    ws1, ws2 = Q.Workspace(H), Q.Workspace(H)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    r1 = Q.run_trials(H, seeds[:512], 0.02, 0, workspace=ws1, stream=s1)
+    r2 = Q.run_trials(H, seeds[512:], 0.02, 0, workspace=ws2, stream=s2)
+    torch.cuda.synchronize()
+    got = np.concatenate([r1.iterations.cpu().numpy(), r2.iterations.cpu().numpy()])
+    assert (got == golden_vectors["c2_iters"][:1024]).all()
+
+
+def test_alist_reader_roundtrip(Q, golden_code, tmp_path):
+    from tests.conftest import write_alist
+    g = golden_code
+    p = os.path.join(tmp_path, "code.alist")
+    write_alist(p, 10240, 5231, g["bit_off"], g["bit_idx"], g["chk_off"], g["chk_idx"])
+    H = Q.HMatrix.from_alist(p)
+    cp, ci, bp, bi = H.adjacency()
+    assert (cp == g["chk_off"]).all() and (ci == g["chk_idx"]).all()
+    assert (bp == g["bit_off"]).all() and (bi == g["bit_idx"]).all()
+    assert not H.is_regular and H.max_bit_nodes_weight == 3 and H.max_check_nodes_weight == 6
