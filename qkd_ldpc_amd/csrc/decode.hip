@@ -27,10 +27,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "qkd_internal.h"
 #include "qkd_math.h"
+#include "qkd_plan.h"
 #include "qkd_rng.h"
 
 namespace qkd {
@@ -63,6 +65,30 @@ struct DecodeArgs {
     double* c2b;
     size_t c2b_stride;
     uint32_t* counter;
+    // diagnostics: per-phase shader-clock cycles summed over workgroups
+    // (thread 0's view between barriers), or nullptr
+    unsigned long long* phase;
+};
+
+// Phase-clock accumulation (diagnostic; a wave-uniform test when off).
+struct PhaseClock {
+    unsigned long long* out;
+    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    long long t = 0;
+    __device__ explicit PhaseClock(unsigned long long* o) : out(threadIdx.x == 0 ? o : nullptr) {
+        if (out) t = clock64();
+    }
+    __device__ __forceinline__ void mark(int k) {
+        if (out) {
+            const long long n = clock64();
+            acc[k] += (unsigned long long)(n - t);
+            t = n;
+        }
+    }
+    __device__ void flush() {
+        if (out)
+            for (int k = 0; k < 5; ++k) atomicAdd(out + k, acc[k]);
+    }
 };
 
 __device__ __forceinline__ double clamp_msg(double v, double thr) {
@@ -84,81 +110,176 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) 
     return r;
 }
 
-// One check's update (qkd_ldpc_algorithm.cpp:220-249 for check j):
-//   b2c_k  = first ? LLR[bit_k] : clamp(total[bit_k] - c2b_k)      (:188, :303-316)
-//   t_k    = tanh(b2c_k / 2)                                       (:224)
-//   P      = (s_j ? -1 : 1) * t_0 * t_1 * ...   (left to right)    (:231-235)
-//   c2b_k  = clamp(2 * atanh(P / t_k))                             (:239-249)
-template <int DC>
-__device__ __forceinline__ void check_update(const DeviceCode& c, const double* total, double* c2b,
-                                             int j, int s, bool first, bool clamp_on, double thr) {
-    const int deg = c.chk_deg[j];
-    double t[DC];
-    double prod = s ? -1.0 : 1.0;
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        if (k < deg) {
-            const int pos = k * c.m_pad + j;
-            const int bit = c.chk_bits[pos];
-            double b = total[bit];
-            if (!first) {
-                b = b - c2b[pos];
-                if (clamp_on) b = clamp_msg(b, thr);
-            }
-            t[k] = qkdm::tanh_ref(b / 2.0);
-            prod *= t[k];
-        }
+
+// LDS layout of decode_kernel (bytes):
+//   total  [n_pad]          binary64 bit totals (the reference's `total`, :256-267)
+//   synm   [n_tasks]        target syndrome per wave task, one bit per lane
+//   tsyn   [m_words]        target syndrome, one bit per check
+//   xsyn   [m_words]        syndrome of the current hard decision (XOR-built)
+//   tval   [NW][64 + DC]    per-wave tanh values for the in-check products
+//   ctl    [4]              frame index, block_any flags
+struct DecodeLds {
+    size_t synm, tsyn, xsyn, tval, ctl, bytes;
+    __host__ __device__ DecodeLds(int n_pad, int n_tasks, int m, int dc) {
+        const int m_words = (m + 31) / 32;
+        synm = (size_t)n_pad * 8;
+        tsyn = synm + (size_t)n_tasks * 8;
+        xsyn = tsyn + (size_t)m_words * 4;
+        tval = (xsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
+        ctl = tval + (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
+        bytes = ctl + 16;
     }
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        if (k < deg) {
-            const int pos = k * c.m_pad + j;
-            double v = 2.0 * qkdm::atanh_ref(prod / t[k]);
-            if (clamp_on) v = clamp_msg(v, thr);
-            c2b[pos] = v;
-        }
-    }
+};
+
+// Bit-phase loads issued together before the ordered sum.
+constexpr int kDvUnroll = 4;
+
+// ---- wave-plan words (qkd_plan.h) ------------------------------------------
+__device__ __forceinline__ uint32_t pw_bit(uint32_t w) { return w & qkdp::kPlanBitMask; }
+__device__ __forceinline__ uint32_t pw_row(uint32_t w) { return (w >> 15) & 31u; }
+__device__ __forceinline__ int pw_start(uint32_t w) { return (int)((w >> 20) & 63u); }
+__device__ __forceinline__ int pw_deg(uint32_t w) { return (int)(w >> 26) + 1; }
+// Parity of the lanes of this lane's check (its segment) in a wave ballot.
+__device__ __forceinline__ int seg_parity(uint64_t ballot, uint32_t w) {
+    const int deg = pw_deg(w);
+    const uint64_t m = deg == 64 ? ~0ull : ((1ull << deg) - 1ull);
+    return __popcll(ballot & (m << pw_start(w))) & 1;
 }
 
-template <int MODE, int DC>
+// One edge of the check phase (qkd_ldpc_algorithm.cpp:220-249):
+//   b2c = FIRST ? LLR_i : clamp(total_i - c2b)                  (:188, :303-316)
+//   t   = tanh(b2c / 2)                                         (:224)
+//   P   = (s_j ? -1 : 1) * t_0 * t_1 * ...  (ascending bits)    (:231-235)
+//   c2b = clamp(2 * atanh(P / t))                               (:239-249)
+// `row` is this wave's LDS row of tanh values (64 + DC doubles, so reads past
+// a segment's end stay inside it and are discarded).
+template <bool FIRST, bool CLAMP, int DC>
+__device__ __forceinline__ double check_edge(double x, double old, uint32_t w, uint64_t sm, int lane,
+                                             double thr, double* row) {
+    if (!FIRST) {
+        x = x - old;
+        if (CLAMP) x = clamp_msg(x, thr);
+    }
+    const double tv = qkdm::tanh_flat(x / 2.0);
+    row[lane] = tv;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int start = pw_start(w);
+    const int deg = pw_deg(w);
+    double o[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) o[k] = row[start + k];
+    double P = ((sm >> lane) & 1ull) ? -1.0 : 1.0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) P = k < deg ? P * o[k] : P;
+    double v = 2.0 * qkdm::atanh_flat(P / tv);
+    if (CLAMP) v = clamp_msg(v, thr);
+    return v;
+}
+
+// The check phase of one iteration for one wave: tasks wave, wave+NW, ...
+// Software-pipelined and unrolled by two so that no loaded value is copied
+// across the loop back-edge. Each half-trip does, in this order:
+//   store the previous task's message  |  issue the look-ahead loads (plan
+//   word two tasks ahead, bit total and stored message one task ahead)  |
+//   compute this task (its operands were loaded one half-trip earlier).
+// vmcnt counts loads and stores in issue order, so a task only ever waits
+// for memory operations that had a whole task of arithmetic to complete.
+// The plan is padded with idle tasks (qkd_plan.h): no bounds tests on the
+// look-ahead loads.
+template <bool FIRST, bool CLAMP, int DC>
+__device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, const uint64_t* synm,
+                                            const double* total, double* __restrict__ c2b, double* row,
+                                            int n_tasks, int n_pad, double thr, int wave, int lane) {
+    constexpr int NW = kDecodeBlock / 64;
+    int t = wave;
+    if (t >= n_tasks) return;
+    const uint32_t* pl = plan + lane;
+    auto msg = [&](uint32_t w) -> double* { return c2b + pw_row(w) * n_pad + pw_bit(w); };
+    uint32_t wa = pl[t * 64];
+    uint32_t wb = pl[(t + NW) * 64];
+    double xa = total[pw_bit(wa)];
+    double oa = FIRST ? 0.0 : *msg(wa);
+    double* pend = nullptr;      // message computed by the previous task, not yet stored
+    double pv = 0.0;
+    for (;;) {
+        if (pend) *pend = pv;
+        const uint32_t wc = pl[(t + 2 * NW) * 64];
+        const double xb = total[pw_bit(wb)];
+        const double ob = FIRST ? 0.0 : *msg(wb);
+        pv = check_edge<FIRST, CLAMP, DC>(xa, oa, wa, synm[t], lane, thr, row);
+        pend = msg(wa);
+        t += NW;
+        if (t >= n_tasks) break;
+        *pend = pv;
+        wa = pl[(t + 2 * NW) * 64];
+        xa = total[pw_bit(wc)];
+        oa = FIRST ? 0.0 : *msg(wc);
+        pv = check_edge<FIRST, CLAMP, DC>(xb, ob, wb, synm[t], lane, thr, row);
+        pend = msg(wb);
+        t += NW;
+        if (t >= n_tasks) break;
+        wb = wa;
+        wa = wc;
+    }
+    *pend = pv;
+}
+
+// Flooding sum-product decode of whole frames, one frame per workgroup at a
+// time (reference sum_product_decoding_irregular, qkd_ldpc_algorithm.cpp:175-345;
+// the regular twin :3-173 is the same arithmetic).
+//
+// Message store: the c2b messages of the frame live bit-major in global memory,
+// c2b[k * n_pad + i] = message from the k-th check (ascending) of bit i, i.e.
+// the reference's c2b[i][k] layout transposed for coalescing (:192-205).
+//
+// Per iteration:
+//  check phase (check_phase above), one edge per lane, wave tasks of whole
+//    checks (qkd_plan.h)
+//  bit phase (:256-267), one bit per lane, coalesced rows:
+//    total_i = LLR_i + c2b[0][i] + c2b[1][i] + ...  (ascending check order)
+//    hard decision z_i = total_i <= 0; if z_i, XOR it into the syndrome bit of
+//    each of its checks (LDS bit array; XOR is order-free, so exact)
+//  syndrome test (:277-285): compare with the target words, block-wide any()
+template <int MODE, int DC, bool CLAMP>
 __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
+    constexpr int NW = kDecodeBlock / 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
-    double* total = reinterpret_cast<double*>(smem);               // [n]
-    uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + (size_t)c.n_pad * 8);  // [0]=frame, [2..3]=any flags
+    const DecodeLds L(c.n_pad, c.n_tasks, c.m, DC);
+    const int m_words = (c.m + 31) / 32;
+    double* total = reinterpret_cast<double*>(smem);
+    uint64_t* synm = reinterpret_cast<uint64_t*>(smem + L.synm);
+    uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
+    uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    double* row = reinterpret_cast<double*>(smem + L.tval) + wave * (64 + DC);
+    const int n_tasks = c.n_tasks;
+    const int n_pad = c.n_pad;
+    const uint32_t* plan = c.plan;
     double* c2b = a.c2b + (size_t)blockIdx.x * a.c2b_stride;
-    const bool clamp_on = a.clamp_on != 0;
+    const double thr = a.thr;
     uint32_t any_k = 0;
     if (tid == 0) { ctl[2] = 0; ctl[3] = 0; }
+    PhaseClock pc(a.phase);
 
     for (;;) {
+        pc.mark(4);
         if (tid == 0) ctl[0] = atomicAdd(a.counter, 1u);
+        for (int w = tid; w < m_words; w += kDecodeBlock) {
+            tsyn[w] = 0;
+            xsyn[w] = 0;
+        }
         __syncthreads();
         const uint32_t f = ctl[0];
         if (f >= a.n_frames) break;
 
-        // ---- prologue: syndrome bits of this thread's checks, channel LLRs
-        uint32_t synmask = 0;
-        {
-            int r = 0;
-            for (int j = tid; j < c.m; j += kDecodeBlock, ++r) {
-                int s;
-                if (MODE == kModeLlr) {
-                    s = a.syn[(size_t)f * c.m + j] != 0;
-                } else {
-                    // calculate_syndrome_irregular on Alice's key (:413-414)
-                    const uint64_t* aw = a.alice_w + (size_t)f * a.words;
-                    const int deg = c.chk_deg[j];
-                    s = 0;
-                    for (int k = 0; k < deg; ++k) {
-                        const int bit = c.chk_bits[k * c.m_pad + j];
-                        s ^= (int)((aw[bit >> 6] >> (bit & 63)) & 1u);
-                    }
-                }
-                synmask |= (uint32_t)s << r;
-            }
-        }
+        // ---- prologue: channel LLRs into LDS (:188 / :400-405); the dummy
+        //      column n of idle plan lanes gets 0
         uint32_t bobmask = 0;
         {
             int r = 0;
@@ -170,48 +291,80 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     const uint64_t w = a.bob_w[(size_t)f * a.words + (i >> 6)];
                     const uint32_t bb = (uint32_t)((w >> (i & 63)) & 1u);
                     bobmask |= bb << r;
-                    l = bb ? -a.log_p : a.log_p;     // qkd_ldpc_algorithm.cpp:402-405
+                    l = bb ? -a.log_p : a.log_p;
                 }
                 total[i] = l;
             }
+            if (tid == 0) total[c.n] = 0.0;
+        }
+        // ---- prologue: target syndrome, per wave task and per check
+        for (int t = wave; t < n_tasks; t += NW) {
+            const int slot = t * 64 + lane;
+            const uint32_t w = plan[slot];
+            const int j = c.plan_chk[slot];
+            int s;
+            if (MODE == kModeLlr) {
+                s = j >= 0 ? (a.syn[(size_t)f * c.m + j] != 0) : 0;
+            } else {
+                // calculate_syndrome_irregular on Alice's key (:413-414)
+                const uint32_t bit = pw_bit(w);
+                int ab = 0;
+                if (j >= 0) ab = (int)((a.alice_w[(size_t)f * a.words + (bit >> 6)] >> (bit & 63)) & 1u);
+                s = seg_parity(__ballot(ab), w);
+            }
+            const uint64_t sm = __ballot(s);
+            if (lane == 0) synm[t] = sm;
+            if (s && j >= 0 && lane == pw_start(w)) atomicOr(&tsyn[j >> 5], 1u << (j & 31));
         }
         __syncthreads();
+        pc.mark(0);
 
-        // ---- iterations (qkd_ldpc_algorithm.cpp:212-330)
+        // ---- iterations (:212-330)
         bool done = false;
         uint32_t it = 0;
         for (; it < a.max_it; ++it) {
-            {
-                int r = 0;
-                for (int j = tid; j < c.m; j += kDecodeBlock, ++r)
-                    check_update<DC>(c, total, c2b, j, (synmask >> r) & 1u, it == 0, clamp_on, a.thr);
-            }
+            if (it == 0)
+                check_phase<true, CLAMP, DC>(plan, synm, total, c2b, row, n_tasks, n_pad, thr, wave, lane);
+            else
+                check_phase<false, CLAMP, DC>(plan, synm, total, c2b, row, n_tasks, n_pad, thr, wave, lane);
             __syncthreads();
-            // bit phase: total_i = LLR_i + sum_k c2b(i,k), ascending checks (:256-267)
+            pc.mark(1);
+            // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
+            // and the hard decision's syndrome (:277, calculate_syndrome_irregular :476-486)
             {
                 int r = 0;
+#pragma unroll 2
                 for (int i = tid; i < c.n; i += kDecodeBlock, ++r) {
                     double acc;
                     if (MODE == kModeLlr) acc = a.llr[(size_t)f * c.n + i];
                     else acc = ((bobmask >> r) & 1u) ? -a.log_p : a.log_p;
                     const int deg = c.bit_deg[i];
-                    for (int k = 0; k < deg; ++k) acc = acc + c2b[c.bit_edge[k * c.n_pad + i]];
+                    double v[kDvUnroll];
+#pragma unroll
+                    for (int k = 0; k < kDvUnroll; ++k) v[k] = k < c.max_dv ? c2b[k * n_pad + i] : 0.0;
+#pragma unroll
+                    for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[k] : acc;
+                    for (int k = kDvUnroll; k < deg; ++k) acc = acc + c2b[k * n_pad + i];
                     total[i] = acc;
+                    if (acc <= 0.0) {
+                        for (int k = 0; k < deg; ++k) {
+                            const int j = c.bit_chk[k * n_pad + i];
+                            atomicXor(&xsyn[j >> 5], 1u << (j & 31));
+                        }
+                    }
                 }
             }
             __syncthreads();
-            // syndrome of the hard decision (total <= 0 -> 1) vs target (:277-285)
+            pc.mark(2);
+            // syndrome test (:285): any word differing from the target
             bool mismatch = false;
-            {
-                int r = 0;
-                for (int j = tid; j < c.m; j += kDecodeBlock, ++r) {
-                    const int deg = c.chk_deg[j];
-                    int d = 0;
-                    for (int k = 0; k < deg; ++k) d ^= (total[c.chk_bits[k * c.m_pad + j]] <= 0.0);
-                    mismatch |= (d != (int)((synmask >> r) & 1u));
-                }
+            for (int w = tid; w < m_words; w += kDecodeBlock) {
+                mismatch |= xsyn[w] != tsyn[w];
+                xsyn[w] = 0;
             }
-            if (!block_any(mismatch, ctl + 2, any_k)) {
+            const bool any_mismatch = block_any(mismatch, ctl + 2, any_k);
+            pc.mark(3);
+            if (!any_mismatch) {
                 done = true;
                 break;
             }
@@ -238,6 +391,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         }
         __syncthreads();
     }
+    pc.flush();
 }
 
 // ---- syndrome ---------------------------------------------------------------
@@ -344,18 +498,27 @@ __global__ void counters_init_kernel(qkd_counters* c) {
 
 using DecodeFn = void (*)(DecodeArgs);
 
-template <int MODE>
-static DecodeFn pick_decode(int max_dc) {
-    if (max_dc <= 6) return decode_kernel<MODE, 6>;
-    if (max_dc <= 8) return decode_kernel<MODE, 8>;
-    return decode_kernel<MODE, 16>;
+// Check-degree buckets: the in-check product reads DC values per lane.
+template <int MODE, bool CLAMP>
+static DecodeFn pick_decode_dc(int max_dc, int* dc) {
+    if (max_dc <= 4) { *dc = 4; return decode_kernel<MODE, 4, CLAMP>; }
+    if (max_dc <= 6) { *dc = 6; return decode_kernel<MODE, 6, CLAMP>; }
+    if (max_dc <= 8) { *dc = 8; return decode_kernel<MODE, 8, CLAMP>; }
+    if (max_dc <= 16) { *dc = 16; return decode_kernel<MODE, 16, CLAMP>; }
+    *dc = 64;
+    return decode_kernel<MODE, 64, CLAMP>;
 }
 
-static size_t decode_lds_bytes(const qkd_code* c) { return (size_t)c->n_pad * 8 + 16; }
+static DecodeFn pick_decode(int mode, bool clamp, int max_dc, int* dc) {
+    if (mode == kModeLlr)
+        return clamp ? pick_decode_dc<kModeLlr, true>(max_dc, dc) : pick_decode_dc<kModeLlr, false>(max_dc, dc);
+    return clamp ? pick_decode_dc<kModeKeys, true>(max_dc, dc) : pick_decode_dc<kModeKeys, false>(max_dc, dc);
+}
+
+static size_t decode_lds_bytes(const qkd_code* c, int dc) { return DecodeLds(c->n_pad, c->n_tasks, c->m, dc).bytes; }
 
 // Resident workgroups of decode_kernel for this code on its device.
-static qkd_status decode_grid(const qkd_code* c, DecodeFn fn, int* grid) {
-    const size_t lds = decode_lds_bytes(c);
+static qkd_status decode_grid(const qkd_code* c, DecodeFn fn, size_t lds, int* grid) {
     QKD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;
     QKD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, kDecodeBlock, lds));
@@ -366,12 +529,12 @@ static qkd_status decode_grid(const qkd_code* c, DecodeFn fn, int* grid) {
 
 qkd_status ws_reserve_decode(qkd_workspace* ws, size_t slots) {
     const qkd_code* c = ws->code;
-    if (!ws->counter) QKD_HIP(hipMalloc(&ws->counter, 64));
+    if (!ws->counter) QKD_HIP(hipMalloc(&ws->counter, 128));
     if (ws->c2b_slots >= slots) return QKD_OK;
     if (ws->c2b) QKD_HIP(hipFree(ws->c2b));
     ws->c2b = nullptr;
     ws->c2b_slots = 0;
-    const size_t bytes = slots * (size_t)c->max_dc * c->m_pad * sizeof(double);
+    const size_t bytes = slots * (size_t)c->max_dv * c->n_pad * sizeof(double);
     if (hipMalloc(&ws->c2b, bytes) != hipSuccess)
         return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate %zu B of c2b scratch", bytes);
     ws->c2b_slots = slots;
@@ -442,19 +605,27 @@ struct WsSession {
 
 static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs& a, int mode,
                                 hipStream_t stream) {
-    DecodeFn fn = mode == kModeLlr ? pick_decode<kModeLlr>(c->max_dc) : pick_decode<kModeKeys>(c->max_dc);
+    int dc = 0;
+    DecodeFn fn = pick_decode(mode, a.clamp_on != 0, c->max_dc, &dc);
+    const size_t lds = decode_lds_bytes(c, dc);
     int grid = 0;
-    qkd_status s = decode_grid(c, fn, &grid);
+    qkd_status s = decode_grid(c, fn, lds, &grid);
     if (s != QKD_OK) return s;
     grid = (int)std::min<size_t>((size_t)grid, a.n_frames);
     s = ws_reserve_decode(ws, (size_t)grid);
     if (s != QKD_OK) return s;
     a.code = c->view();
     a.c2b = ws->c2b;
-    a.c2b_stride = (size_t)c->max_dc * c->m_pad;
+    a.c2b_stride = (size_t)c->max_dv * c->n_pad;
     a.counter = ws->counter;
     QKD_HIP(hipMemsetAsync(ws->counter, 0, 4, stream));
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kDecodeBlock), decode_lds_bytes(c), stream, a);
+    static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;
+    a.phase = nullptr;
+    if (timing) {
+        a.phase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 64);
+        QKD_HIP(hipMemsetAsync(a.phase, 0, 64, stream));
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kDecodeBlock), lds, stream, a);
     QKD_HIP(hipGetLastError());
     return QKD_OK;
 }
@@ -630,6 +801,15 @@ qkd_status qkd_keygen_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t
     hipLaunchKernelGGL(unpack_kernel, dim3(blocks_for(nb, 256)), dim3(256), 0, (hipStream_t)stream,
                        ws->bob_w, (uint32_t)c->n, words, (uint32_t)n_frames, bob);
     QKD_HIP(hipGetLastError());
+    return QKD_OK;
+}
+
+qkd_status qkd_debug_phase_cycles(qkd_workspace* ws, uint64_t* cycles5) {
+    if (!ws || !cycles5) return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    if (!ws->counter) return set_error(QKD_ERR_INVALID_ARG, "workspace has not decoded yet");
+    DeviceGuard g(ws->device);
+    QKD_HIP(hipDeviceSynchronize());
+    QKD_HIP(hipMemcpy(cycles5, reinterpret_cast<char*>(ws->counter) + 64, 40, hipMemcpyDeviceToHost));
     return QKD_OK;
 }
 

@@ -11,6 +11,7 @@
 #include <sstream>
 
 #include "qkd_internal.h"
+#include "qkd_plan.h"
 #include "qkd_rng.h"
 
 namespace qkd {
@@ -36,11 +37,15 @@ static void free_device(qkd_code* c) {
     DeviceGuard g(c->device);
     if (c->d_chk_bits) (void)hipFree(c->d_chk_bits);
     if (c->d_chk_deg) (void)hipFree(c->d_chk_deg);
-    if (c->d_bit_edge) (void)hipFree(c->d_bit_edge);
+    if (c->d_bit_chk) (void)hipFree(c->d_bit_chk);
     if (c->d_bit_deg) (void)hipFree(c->d_bit_deg);
+    if (c->d_plan) (void)hipFree(c->d_plan);
+    if (c->d_plan_chk) (void)hipFree(c->d_plan_chk);
+    c->d_plan = nullptr;
+    c->d_plan_chk = nullptr;
     c->d_chk_bits = nullptr;
     c->d_chk_deg = nullptr;
-    c->d_bit_edge = nullptr;
+    c->d_bit_chk = nullptr;
     c->d_bit_deg = nullptr;
 }
 
@@ -75,7 +80,10 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     for (int32_t i = 0; i < n; ++i) max_dv = std::max(max_dv, bdeg[i]);
     if (max_dc > kMaxCheckDegree)
         return set_error(QKD_ERR_UNSUPPORTED, "check degree %d exceeds %d", max_dc, kMaxCheckDegree);
-    if (max_dv > 255) return set_error(QKD_ERR_UNSUPPORTED, "bit degree %d exceeds 255", max_dv);
+    if (max_dv > qkdp::kPlanMaxBitDegree)
+        return set_error(QKD_ERR_UNSUPPORTED, "bit degree %d exceeds %d", max_dv, qkdp::kPlanMaxBitDegree);
+    if (n > qkdp::kPlanMaxBits)
+        return set_error(QKD_ERR_UNSUPPORTED, "N=%d exceeds the plan limit %d", n, qkdp::kPlanMaxBits);
     if (n > kMaxBitsLds)
         return set_error(QKD_ERR_UNSUPPORTED, "N=%d exceeds the LDS-resident limit %d", n, kMaxBitsLds);
 
@@ -92,12 +100,13 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     for (int32_t i = 0; i < n; ++i) c->bit_ptr[i + 1] = c->bit_ptr[i] + bdeg[i];
     c->bit_idx.assign(e, 0);
     std::vector<int32_t> fill(c->bit_ptr.begin(), c->bit_ptr.end() - 1);
-    c->n_pad = round_up(n, 64);
+    c->n_pad = round_up(n + 1, 64);   // column n: dummy target of idle plan lanes
     c->m_pad = round_up(m, 64);
     std::vector<int32_t> chk_bits((size_t)max_dc * c->m_pad, -1);
     std::vector<uint8_t> chk_deg(m, 0);
-    std::vector<int32_t> bit_edge((size_t)max_dv * c->n_pad, -1);
+    std::vector<int32_t> bit_chk((size_t)max_dv * c->n_pad, -1);
     std::vector<uint8_t> bit_deg(n, 0);
+    std::vector<int32_t> krow(e, 0);
     for (int32_t j = 0; j < m; ++j) {
         chk_deg[j] = (uint8_t)(cptr[j + 1] - cptr[j]);
         for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) {
@@ -106,9 +115,14 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
             chk_bits[(size_t)slot * c->m_pad + j] = b;
             const int32_t bk = fill[b] - c->bit_ptr[b];
             c->bit_idx[fill[b]++] = j;
-            bit_edge[(size_t)bk * c->n_pad + b] = slot * c->m_pad + j;
+            bit_chk[(size_t)bk * c->n_pad + b] = j;
+            krow[k] = bk;
         }
     }
+    qkdp::WavePlan plan;
+    if (!qkdp::build_wave_plan(n, m, cptr, cidx, krow.data(), plan))
+        return set_error(QKD_ERR_UNSUPPORTED, "check degree outside [1, %d]", qkdp::kPlanMaxDegree);
+    c->n_tasks = plan.n_tasks;
     bool reg = true;
     for (int32_t i = 0; i < n; ++i) {
         bit_deg[i] = (uint8_t)bdeg[i];
@@ -126,14 +140,20 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     QKD_HIP(hipDeviceGetAttribute(&c->cu_count, hipDeviceAttributeMultiprocessorCount, device));
     QKD_HIP(hipMalloc(&c->d_chk_bits, chk_bits.size() * sizeof(int32_t)));
     QKD_HIP(hipMalloc(&c->d_chk_deg, chk_deg.size()));
-    QKD_HIP(hipMalloc(&c->d_bit_edge, bit_edge.size() * sizeof(int32_t)));
+    QKD_HIP(hipMalloc(&c->d_bit_chk, bit_chk.size() * sizeof(int32_t)));
     QKD_HIP(hipMalloc(&c->d_bit_deg, bit_deg.size()));
     QKD_HIP(hipMemcpy(c->d_chk_bits, chk_bits.data(), chk_bits.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_chk_deg, chk_deg.data(), chk_deg.size(), hipMemcpyHostToDevice));
-    QKD_HIP(hipMemcpy(c->d_bit_edge, bit_edge.data(), bit_edge.size() * sizeof(int32_t),
+    QKD_HIP(hipMemcpy(c->d_bit_chk, bit_chk.data(), bit_chk.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_bit_deg, bit_deg.data(), bit_deg.size(), hipMemcpyHostToDevice));
+    QKD_HIP(hipMalloc(&c->d_plan, plan.word.size() * sizeof(uint32_t)));
+    QKD_HIP(hipMalloc(&c->d_plan_chk, plan.chk.size() * sizeof(int32_t)));
+    QKD_HIP(hipMemcpy(c->d_plan, plan.word.data(), plan.word.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice));
+    QKD_HIP(hipMemcpy(c->d_plan_chk, plan.chk.data(), plan.chk.size() * sizeof(int32_t),
+                      hipMemcpyHostToDevice));
     return QKD_OK;
 }
 

@@ -14,24 +14,31 @@ namespace qkd {
 
 // Threads per decode workgroup: one workgroup decodes one frame at a time.
 constexpr int kDecodeBlock = 1024;
-// Largest check degree the register-resident check update handles.
-constexpr int kMaxCheckDegree = 16;
+// Largest check degree: one check's edges fit one wavefront (qkd_plan.h).
+constexpr int kMaxCheckDegree = 64;
 // The per-frame bit totals live in LDS as binary64: N <= this.
 constexpr int kMaxBitsLds = 20480;
 
 // Device-resident, immutable view of H.
 //   chk_bits[k * m_pad + j]  bit index of slot k of check j (ascending), -1 pad
-//   bit_edge[k * n_pad + i]  c2b storage slot (k' * m_pad + j) of the k-th
-//                            check of bit i (ascending), -1 pad
-// Slot-major ("ELL") layouts keep lane-consecutive checks / bits on
-// consecutive addresses.
+//                            (thread-per-check syndrome kernel)
+//   plan[s], plan_chk[s]     the check-phase wave plan (qkd_plan.h): slot
+//                            s = task*64 + lane holds one edge
+//   bit_chk[k * n_pad + i]   k-th check of bit i (ascending), -1 pad; c2b
+//                            messages are stored per frame bit-major in the
+//                            same [k][i] shape
+// Slot-major ("ELL") layouts keep lane-consecutive bits on consecutive
+// addresses.
 struct DeviceCode {
     int32_t n, m, e;
     int32_t n_pad, m_pad;
     int32_t max_dv, max_dc;
+    int32_t n_tasks;
     const int32_t* chk_bits;
     const uint8_t* chk_deg;
-    const int32_t* bit_edge;
+    const uint32_t* plan;
+    const int32_t* plan_chk;
+    const int32_t* bit_chk;
     const uint8_t* bit_deg;
 };
 
@@ -61,17 +68,20 @@ struct qkd_code {
     int32_t n = 0, m = 0, e = 0;
     int32_t max_dv = 0, max_dc = 0, is_regular = 0;
     int32_t n_pad = 0, m_pad = 0;
+    int32_t n_tasks = 0;
     std::vector<int32_t> check_ptr, check_idx, bit_ptr, bit_idx;
     int32_t* d_chk_bits = nullptr;
     uint8_t* d_chk_deg = nullptr;
-    int32_t* d_bit_edge = nullptr;
+    int32_t* d_bit_chk = nullptr;
     uint8_t* d_bit_deg = nullptr;
+    uint32_t* d_plan = nullptr;
+    int32_t* d_plan_chk = nullptr;
     int cu_count = 0;
     qkd_workspace* default_ws = nullptr;
 
     qkd::DeviceCode view() const {
-        return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc,
-                               d_chk_bits, d_chk_deg, d_bit_edge, d_bit_deg};
+        return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, n_tasks,
+                               d_chk_bits, d_chk_deg, d_plan, d_plan_chk, d_bit_chk, d_bit_deg};
     }
 };
 

@@ -263,4 +263,170 @@ QKD_HD double atanh_ref(double x) {
     return __builtin_copysign(t, x);
 }
 
+
+// ===========================================================================
+// Branch-free ("flat") forms for the kernels.
+//
+// The functions above follow the published code path by path. On a 64-lane
+// wavefront every value-dependent `if` whose lanes disagree executes both
+// sides, and tanh/atanh each inline TWO copies of expm1/log1p (one per
+// magnitude branch), so a divergent wave pays for four transcendentals per
+// call. The forms below compute each result with the same sequence of
+// binary64 operations on the same operands as the path the reference would
+// take, but select operands and results instead of branching: one expm1 /
+// log1p body per call, one division per quotient. Every select picks between
+// values that the reference computes identically, so results are bitwise
+// equal to tanh_ref / atanh_ref for every input (tests/native/math_check.cpp
+// checks them against glibc and against the path-by-path forms).
+// ===========================================================================
+
+QKD_HD double sel(bool p, double a, double b) { return p ? a : b; }
+
+// expm1 restricted to the arguments tanh feeds it:
+//   a in [-2, -2^-54]  (tanh of 2^-55 <= |x| < 1: expm1(-2|x|))
+//   a in [ 2,  44)     (tanh of 1 <= |x| < 22:    expm1( 2|x|))
+// On this domain the reference's expm1 takes only these paths:
+//   k = 0 (|a| <= ln2/2), k = -1 (ln2/2 < |a| < 1.5 ln2, a < 0), general
+//   k in {-3,-2} or [3, 64]; no overflow, no k = 1, no k = 1024.
+QKD_HD double expm1_tanh_domain(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double Q1 = -3.33333333333331316428e-02;
+    const double Q2 = 1.58730158725481460165e-03;
+    const double Q3 = -7.93650757867487942473e-05;
+    const double Q4 = 4.00821782732936239552e-06;
+    const double Q5 = -2.01099218183624371326e-07;
+
+    const uint32_t ahx = (uint32_t)hi32(x) & 0x7fffffffu;
+    const bool neg = x < 0.0;
+    const bool red = ahx > 0x3fd62e42u;          // |x| > ln2/2: reduce
+    const bool km1 = ahx < 0x3FF0A2B2u;          // |x| < 1.5 ln2 (negative side only here)
+    // general k = (int)(invln2*x -+ 0.5), hi = x - k*ln2_hi, lo = k*ln2_lo
+    const int kg = (int)(invln2 * x + (neg ? -0.5 : 0.5));
+    const double tg = (double)kg;
+    const double hi_g = x - tg * ln2_hi;
+    const double lo_g = tg * ln2_lo;
+    const double hi = red ? (km1 ? x + ln2_hi : hi_g) : x;
+    const double lo = red ? (km1 ? -ln2_lo : lo_g) : 0.0;
+    const int k = red ? (km1 ? -1 : kg) : 0;
+    const double xr = hi - lo;                   // == x when k == 0
+    const double c = (hi - xr) - lo;
+
+    const double hfx = 0.5 * xr;
+    const double hxs = xr * hfx;
+    const double R1 = 1.0 + hxs * Q1;
+    const double h2 = hxs * hxs;
+    const double R2 = Q2 + hxs * Q3;
+    const double h4 = h2 * h2;
+    const double R3 = Q4 + hxs * Q5;
+    const double r1 = R1 + h2 * R2 + h4 * R3;
+    const double t = 3.0 - r1 * hfx;
+    const double e = hxs * ((r1 - t) / (6.0 - xr * t));
+
+    const double res0 = xr - (xr * e - hxs);                 // k == 0
+    const double e2 = (xr * (e - c) - c) - hxs;              // k != 0
+    const double resm1 = 0.5 * (xr - e2) - 0.5;              // k == -1
+    const bool big = k <= -2 || k > 56;
+    const int ks = k < 0 ? 0 : (k > 31 ? 31 : k);
+    const double t1 = from_bits((uint64_t)(0x3ff00000u - (0x200000u >> ks)) << 32);      // 1 - 2^-k
+    const double t2 = from_bits((uint64_t)((uint32_t)(0x3ff - k) << 20) << 32);          // 2^-k
+    const double a12 = (big ? 1.0 : t1) - (e2 - xr);         // k <= -2 | k > 56 | 2 <= k < 20
+    const double a3 = (xr - (e2 + t2)) + 1.0;                // 20 <= k <= 56
+    const double a = (big || k < 20) ? a12 : a3;
+    const double y = set_hi32(a, (uint32_t)hi32(a) + ((uint32_t)k << 20));
+    const double resg = big ? y - 1.0 : y;
+    return k == 0 ? res0 : (k == -1 ? resm1 : resg);
+}
+
+QKD_HD double tanh_flat(double x) {
+    const int32_t jx = hi32(x);
+    const int32_t ix = jx & 0x7fffffff;
+    const double ax = __builtin_fabs(x);
+    const bool ge1 = ix >= 0x3ff00000;
+    const bool body = ix >= 0x3c800000 && ix < 0x40360000;     // 2^-55 <= |x| < 22
+    const double a = body ? (ge1 ? 2.0 * ax : -2.0 * ax) : 2.0;
+    const double t = expm1_tanh_domain(a);
+    const double q = (ge1 ? 2.0 : -t) / (t + 2.0);            // 2/(t+2) or -t/(t+2)
+    double z = ge1 ? 1.0 - q : q;
+    z = ix >= 0x40360000 ? 1.0 : z;                           // |x| >= 22
+    double r = jx >= 0 ? z : -z;
+    r = ix < 0x3c800000 ? x * (1.0 + x) : r;                  // tiny and +-0 (x*(1+x) == x)
+    const double sp = x != x ? x + x : (jx >= 0 ? 1.0 : -1.0); // NaN / +-inf
+    return ix >= 0x7ff00000 ? sp : r;
+}
+
+// log1p restricted to the arguments atanh feeds it: x in [2^-27, 2^54],
+// finite and positive. Paths used: k = 0 (x < 0.41422), and k != 0 with
+// u = 1 + x (x < 2^53) or u = x (x >= 2^53); either with |f| < 2^-20 tails.
+QKD_HD double log1p_atanh_domain(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double Lp1 = 6.666666666666735130e-01;
+    const double Lp2 = 3.999999999940941908e-01;
+    const double Lp3 = 2.857142874366239149e-01;
+    const double Lp4 = 2.222219843214978396e-01;
+    const double Lp5 = 1.818357216161805012e-01;
+    const double Lp6 = 1.531383769920937332e-01;
+    const double Lp7 = 1.479819860511658591e-01;
+
+    const int32_t hx = hi32(x);
+    const bool k0 = hx < 0x3FDA827A;                          // x < 0.41422: k = 0, f = x
+    const bool huge = hx >= 0x43400000;                       // x >= 2^53: u = x, c = 0
+    const double u1 = 1.0 + x;
+    double u = huge ? x : u1;
+    int32_t hu = hi32(u);
+    int32_t k = (hu >> 20) - 1023;
+    double c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);
+    c = huge ? 0.0 : c / u;
+    hu &= 0x000fffff;
+    const bool lowm = hu < 0x6a09e;
+    u = set_hi32(u, (uint32_t)hu | (lowm ? 0x3ff00000u : 0x3fe00000u));
+    k = lowm ? k : k + 1;
+    hu = lowm ? hu : (0x00100000 - hu) >> 2;
+    double f = u - 1.0;
+    // k = 0 path
+    f = k0 ? x : f;
+    k = k0 ? 0 : k;
+    hu = k0 ? 1 : hu;
+    c = k0 ? 0.0 : c;
+
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)k;
+    // |f| < 2^-20 tails (hu == 0)
+    const double R0 = hfsq * (1.0 - 0.66666666666666666 * f);
+    const double tail_f0 = k == 0 ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
+    const double tail_r = k == 0 ? f - R0 : dk * ln2_hi - ((R0 - (dk * ln2_lo + c)) - f);
+    const double tail = f == 0.0 ? tail_f0 : tail_r;
+    // main
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double R1 = z * Lp1;
+    const double z2 = z * z;
+    const double R2 = Lp2 + z * Lp3;
+    const double z4 = z2 * z2;
+    const double R3 = Lp4 + z * Lp5;
+    const double z6 = z4 * z2;
+    const double R4 = Lp6 + z * Lp7;
+    const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+    const double m = k == 0 ? f - (hfsq - s * (hfsq + R))
+                            : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+    return hu == 0 ? tail : m;
+}
+
+QKD_HD double atanh_flat(double x) {
+    const double xa = __builtin_fabs(x);
+    const bool small = xa < 0.5;
+    const double t = xa + xa;
+    const double q = (small ? t * xa : t) / (1.0 - xa);      // t*xa/(1-xa) or (xa+xa)/(1-xa)
+    const double arg = small ? t + q : q;
+    const bool body = xa >= 0x1.0p-28 && xa < 1.0;            // false for NaN
+    const double r = 0.5 * log1p_atanh_domain(body ? arg : 1.0);
+    const double res = __builtin_copysign(r, x);
+    // |x| >= 1 or NaN: +-1 -> +-inf, |x| > 1 -> NaN, NaN -> NaN
+    const double inf = __builtin_copysign(__builtin_inf(), x);
+    const double sp = xa == 1.0 ? inf : (x != x ? x + x : __builtin_nan(""));
+    return xa < 0x1.0p-28 ? x : (body ? res : sp);
+}
+
 }  // namespace qkdm

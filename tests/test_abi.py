@@ -88,8 +88,8 @@ def test_code_validation_statuses(N):
     assert st == N.ERR_BAD_CODE                      # check_ptr[0] != 0
     st, _ = _create(N, 0, 2, [0, 2, 4], [0, 1, 2, 3])
     assert st == N.ERR_INVALID_ARG
-    st, _ = _create(N, 40, 1, [0, 20], list(range(20)))
-    assert st == N.ERR_UNSUPPORTED                   # check degree > 16
+    st, _ = _create(N, 80, 1, [0, 65], list(range(65)))
+    assert st == N.ERR_UNSUPPORTED                   # check degree > 64 (one wavefront)
 
 
 def test_valid_code_without_gpu_reports_device_error(N):
