@@ -37,6 +37,9 @@
 
 namespace qkd {
 
+// Largest check degree the first-iteration table covers.
+constexpr int kFirstTableDeg = 16;
+
 enum DecodeMode : int {
     kModeLlr = 0,  // qkd_decode_batch: caller LLRs + syndrome bytes
     kModeKeys = 1  // QKD_LDPC path: packed alice/bob keys, LLR = +-log_p
@@ -56,6 +59,12 @@ struct DecodeArgs {
     const uint64_t* bob_w;
     uint32_t words;
     double log_p;
+    // First-iteration message table (kModeKeys): with every channel LLR equal
+    // to +-log_p, the first check phase is a function of signs and degrees
+    // only (see first_check_phase); first_c2b[d] = its message magnitude for
+    // a check of degree d. Used when first_table != 0.
+    int first_table;
+    double first_c2b[kFirstTableDeg + 1];
     // outputs
     uint8_t* bits_out;
     uint32_t* iters;
@@ -117,16 +126,18 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) 
 //   tsyn   [m_words]        target syndrome, one bit per check
 //   xsyn   [m_words]        syndrome of the current hard decision (XOR-built)
 //   tval   [NW][64 + DC]    per-wave tanh values for the in-check products
+//   ctab   [kFirstTableDeg+1] first-iteration message magnitudes by degree
 //   ctl    [4]              frame index, block_any flags
 struct DecodeLds {
-    size_t synm, tsyn, xsyn, tval, ctl, bytes;
+    size_t synm, tsyn, xsyn, tval, ctab, ctl, bytes;
     __host__ __device__ DecodeLds(int n_pad, int n_tasks, int m, int dc) {
         const int m_words = (m + 31) / 32;
         synm = (size_t)n_pad * 8;
         tsyn = synm + (size_t)n_tasks * 8;
         xsyn = tsyn + (size_t)m_words * 4;
         tval = (xsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
-        ctl = tval + (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
+        ctab = tval + (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
+        ctl = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         bytes = ctl + 16;
     }
 };
@@ -226,6 +237,32 @@ __device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, c
     *pend = pv;
 }
 
+// First check phase of the QKD path (QKD_LDPC_irregular, :398-425 -> :220-249
+// at it = 0), where b2c = LLR_i = bob_i ? -log_p : +log_p for every edge. Then
+//   t_i = tanh(LLR_i / 2) = sign_i * T,  T = |tanh(log_p / 2)|  (tanh is odd)
+//   P   = (s_j ? -1 : 1) * t_0 * ... * t_{d-1}: binary64 products round on
+//         magnitudes only, so |P| = M_d = (((T * T) * T) ...) and
+//         sign(P) = s_j ^ sign_0 ^ ... ^ sign_{d-1}
+//   c2b = clamp(2 atanh(P / t_i)) = sign(P) ^ sign_i times
+//         C_d = clamp(2 atanh(M_d / T))            (atanh and clamp are odd)
+// so every first-iteration message is +-C_d, bit for bit; the host evaluates
+// C_d with the same tanh/atanh restatement (decode_keys). sign_i is the sign
+// bit of the LLR in `total` (also right for log_p <= 0 and for +-0).
+__device__ __forceinline__ void first_check_phase(const uint32_t* __restrict__ plan, const uint64_t* synm,
+                                                  const double* total, const double* ctab,
+                                                  double* __restrict__ c2b, int n_tasks, int n_pad, int wave,
+                                                  int lane) {
+    constexpr int NW = kDecodeBlock / 64;
+    for (int t = wave; t < n_tasks; t += NW) {
+        const uint32_t w = plan[t * 64 + lane];
+        const uint32_t bit = pw_bit(w);
+        const uint32_t sg = (uint32_t)qkdm::hi32(total[bit]) >> 31;
+        const uint32_t sp = (uint32_t)((synm[t] >> lane) & 1ull) ^ (uint32_t)seg_parity(__ballot(sg), w);
+        const double cm = ctab[pw_deg(w)];
+        c2b[pw_row(w) * n_pad + bit] = (sp ^ sg) ? -cm : cm;
+    }
+}
+
 // Flooding sum-product decode of whole frames, one frame per workgroup at a
 // time (reference sum_product_decoding_irregular, qkd_ldpc_algorithm.cpp:175-345;
 // the regular twin :3-173 is the same arithmetic).
@@ -254,6 +291,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
+    double* ctab = reinterpret_cast<double*>(smem + L.ctab);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -265,6 +303,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     const double thr = a.thr;
     uint32_t any_k = 0;
     if (tid == 0) { ctl[2] = 0; ctl[3] = 0; }
+    if (MODE == kModeKeys && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
     PhaseClock pc(a.phase);
 
     for (;;) {
@@ -323,7 +362,9 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         bool done = false;
         uint32_t it = 0;
         for (; it < a.max_it; ++it) {
-            if (it == 0)
+            if (it == 0 && MODE == kModeKeys && a.first_table)
+                first_check_phase(plan, synm, total, ctab, c2b, n_tasks, n_pad, wave, lane);
+            else if (it == 0)
                 check_phase<true, CLAMP, DC>(plan, synm, total, c2b, row, n_tasks, n_pad, thr, wave, lane);
             else
                 check_phase<false, CLAMP, DC>(plan, synm, total, c2b, row, n_tasks, n_pad, thr, wave, lane);
@@ -728,6 +769,19 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     a.bob_w = ws->bob_w;
     a.words = (uint32_t)((c->n + 63) / 64);
     a.log_p = std::log((1. - q) / q);          // host glibc log, qkd_ldpc_algorithm.cpp:400
+    // first-iteration message magnitudes by check degree (first_check_phase)
+    a.first_table = c->max_dc <= kFirstTableDeg ? 1 : 0;
+    if (a.first_table) {
+        const double T = std::fabs(qkdm::tanh_flat(a.log_p / 2.0));
+        double M = 1.0;
+        a.first_c2b[0] = 0.0;
+        for (int d = 1; d <= kFirstTableDeg; ++d) {
+            M = M * T;
+            double v = 2.0 * qkdm::atanh_flat(M / T);
+            if (a.clamp_on) v = v > thr ? thr : (v < -thr ? -thr : v);
+            a.first_c2b[d] = v;
+        }
+    }
     a.bits_out = bits_out;
     a.iters = iters;
     a.sp_ok = sp_ok;
