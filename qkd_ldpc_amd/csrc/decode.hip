@@ -65,6 +65,9 @@ struct DecodeArgs {
     // a check of degree d. Used when first_table != 0.
     int first_table;
     double first_c2b[kFirstTableDeg + 1];
+    // Second-iteration tanh table (kModeKeys, needs first_table): entries,
+    // 0 when off (see second_table_fill).
+    int tab2_entries;
     // outputs
     uint8_t* bits_out;
     uint32_t* iters;
@@ -127,17 +130,21 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) 
 //   xsyn   [m_words]        syndrome of the current hard decision (XOR-built)
 //   tval   [NW][64 + DC]    per-wave tanh values for the in-check products
 //   ctab   [kFirstTableDeg+1] first-iteration message magnitudes by degree
+//   tab2   [tab2_entries]   second-iteration tanh table
+//   t2idx  [n_pad]          per-bit base index into tab2 (uint16)
 //   ctl    [4]              frame index, block_any flags
 struct DecodeLds {
-    size_t synm, tsyn, xsyn, tval, ctab, ctl, bytes;
-    __host__ __device__ DecodeLds(int n_pad, int n_tasks, int m, int dc) {
+    size_t synm, tsyn, xsyn, tval, ctab, tab2, t2idx, ctl, bytes;
+    __host__ __device__ DecodeLds(int n_pad, int n_tasks, int m, int dc, int tab2_entries) {
         const int m_words = (m + 31) / 32;
         synm = (size_t)n_pad * 8;
         tsyn = synm + (size_t)n_tasks * 8;
         xsyn = tsyn + (size_t)m_words * 4;
         tval = (xsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
         ctab = tval + (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
-        ctl = ctab + (size_t)(kFirstTableDeg + 1) * 8;
+        tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
+        t2idx = tab2 + (size_t)tab2_entries * 8;
+        ctl = (t2idx + (tab2_entries ? (size_t)n_pad * 2 : 0) + 15) & ~(size_t)15;
         bytes = ctl + 16;
     }
 };
@@ -164,14 +171,21 @@ __device__ __forceinline__ int seg_parity(uint64_t ballot, uint32_t w) {
 //   c2b = clamp(2 * atanh(P / t))                               (:239-249)
 // `row` is this wave's LDS row of tanh values (64 + DC doubles, so reads past
 // a segment's end stay inside it and are discarded).
-template <bool FIRST, bool CLAMP, int DC>
+// Where a check phase takes its incoming tanh values from.
+enum CheckSrc : int {
+    kSrcGeneral = 0,   // tanh(clamp(total_i - c2b) / 2)
+    kSrcFirst = 1,     // first iteration: tanh(LLR_i / 2)
+    kSrcTable = 2      // second QKD iteration: looked up (second_table_index)
+};
+
+template <int SRC, bool CLAMP, int DC>
 __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, uint64_t sm, int lane,
                                              double thr, double* row) {
-    if (!FIRST) {
+    if (SRC == kSrcGeneral) {
         x = x - old;
         if (CLAMP) x = clamp_msg(x, thr);
     }
-    const double tv = qkdm::tanh_flat(x / 2.0);
+    const double tv = SRC == kSrcTable ? x : qkdm::tanh_flat(x / 2.0);
     row[lane] = tv;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -199,35 +213,41 @@ __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, u
 // for memory operations that had a whole task of arithmetic to complete.
 // The plan is padded with idle tasks (qkd_plan.h): no bounds tests on the
 // look-ahead loads.
-template <bool FIRST, bool CLAMP, int DC>
+template <int SRC, bool CLAMP, int DC>
 __device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, const uint64_t* synm,
-                                            const double* total, double* __restrict__ c2b, double* row,
+                                            const double* total, const uint16_t* t2idx, const double* tab2,
+                                            double* __restrict__ c2b, double* row,
                                             int n_tasks, int n_pad, double thr, int wave, int lane) {
     constexpr int NW = kDecodeBlock / 64;
+    constexpr bool FIRST = SRC != kSrcGeneral;    // no stored message is read
     int t = wave;
     if (t >= n_tasks) return;
     const uint32_t* pl = plan + lane;
     auto msg = [&](uint32_t w) -> double* { return c2b + pw_row(w) * n_pad + pw_bit(w); };
+    // the incoming value: a bit total, or (kSrcTable) the tabulated tanh
+    auto src = [&](uint32_t w) -> double {
+        return SRC == kSrcTable ? tab2[t2idx[pw_bit(w)] + pw_row(w)] : total[pw_bit(w)];
+    };
     uint32_t wa = pl[t * 64];
     uint32_t wb = pl[(t + NW) * 64];
-    double xa = total[pw_bit(wa)];
+    double xa = src(wa);
     double oa = FIRST ? 0.0 : *msg(wa);
     double* pend = nullptr;      // message computed by the previous task, not yet stored
     double pv = 0.0;
     for (;;) {
         if (pend) *pend = pv;
         const uint32_t wc = pl[(t + 2 * NW) * 64];
-        const double xb = total[pw_bit(wb)];
+        const double xb = src(wb);
         const double ob = FIRST ? 0.0 : *msg(wb);
-        pv = check_edge<FIRST, CLAMP, DC>(xa, oa, wa, synm[t], lane, thr, row);
+        pv = check_edge<SRC, CLAMP, DC>(xa, oa, wa, synm[t], lane, thr, row);
         pend = msg(wa);
         t += NW;
         if (t >= n_tasks) break;
         *pend = pv;
         wa = pl[(t + 2 * NW) * 64];
-        xa = total[pw_bit(wc)];
+        xa = src(wc);
         oa = FIRST ? 0.0 : *msg(wc);
-        pv = check_edge<FIRST, CLAMP, DC>(xb, ob, wb, synm[t], lane, thr, row);
+        pv = check_edge<SRC, CLAMP, DC>(xb, ob, wb, synm[t], lane, thr, row);
         pend = msg(wb);
         t += NW;
         if (t >= n_tasks) break;
@@ -235,6 +255,49 @@ __device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, c
         wa = wc;
     }
     *pend = pv;
+}
+
+// Second check phase of the QKD path. After the first iteration every message
+// is +-C_d (first_check_phase), so bit i's total is
+//   total_i = ((LLR_i + c_0) + c_1) + ...    c_k = sign_k * C_{d_k}   (:256-267)
+// and its second-iteration incoming value for its k-th check is
+//   t = tanh(clamp(total_i - c_k) / 2)                            (:303-316, :224)
+// a function of (the degrees d_k of bit i's checks, bob_i, sign_0.., k). The
+// table holds it for every degree pattern p, sign code and row k:
+//   tab2[p * stride + code * max_dv + k],  code = bob_i | sign_k << (1 + k)
+// computed with the same binary64 operations in the same order. The
+// iteration-1 bit phase records each bit's base index (second_table_index).
+template <bool CLAMP>
+__device__ void second_table_fill(const DeviceCode& c, const double* ctab, double log_p, double thr,
+                                  double* tab2, int entries) {
+    const int dvm = c.max_dv;
+    const int stride = tab2_stride(dvm);
+    for (int e = threadIdx.x; e < entries; e += kDecodeBlock) {
+        const int p = e / stride;
+        const int r = e - p * stride;
+        const int code = r / dvm;
+        const int k = r - code * dvm;
+        const uint8_t* degs = c.pat_deg + p * dvm;
+        double total = (code & 1) ? -log_p : log_p;
+        double ck = 0.0;
+        int dv = 0;
+        for (int m = 0; m < dvm; ++m) {
+            if (degs[m] == 0) break;
+            const double cm = ctab[degs[m]];
+            const double v = ((code >> (1 + m)) & 1) ? -cm : cm;
+            total = total + v;
+            if (m == k) ck = v;
+            dv = m + 1;
+        }
+        double y = 0.0;
+        if (k < dv) {
+            double b = total - ck;
+            if (CLAMP) b = clamp_msg(b, thr);
+            y = qkdm::tanh_flat(b / 2.0);
+        }
+        tab2[e] = y;
+    }
+    __syncthreads();
 }
 
 // First check phase of the QKD path (QKD_LDPC_irregular, :398-425 -> :220-249
@@ -284,7 +347,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     constexpr int NW = kDecodeBlock / 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
-    const DecodeLds L(c.n_pad, c.n_tasks, c.m, DC);
+    const DecodeLds L(c.n_pad, c.n_tasks, c.m, DC, a.tab2_entries);
     const int m_words = (c.m + 31) / 32;
     double* total = reinterpret_cast<double*>(smem);
     uint64_t* synm = reinterpret_cast<uint64_t*>(smem + L.synm);
@@ -292,6 +355,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
+    double* tab2 = reinterpret_cast<double*>(smem + L.tab2);
+    uint16_t* t2idx = reinterpret_cast<uint16_t*>(smem + L.t2idx);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -304,6 +369,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     uint32_t any_k = 0;
     if (tid == 0) { ctl[2] = 0; ctl[3] = 0; }
     if (MODE == kModeKeys && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
+    if (MODE == kModeKeys && a.tab2_entries) {
+        __syncthreads();
+        second_table_fill<CLAMP>(c, ctab, a.log_p, thr, tab2, a.tab2_entries);
+    }
     PhaseClock pc(a.phase);
 
     for (;;) {
@@ -365,9 +434,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             if (it == 0 && MODE == kModeKeys && a.first_table)
                 first_check_phase(plan, synm, total, ctab, c2b, n_tasks, n_pad, wave, lane);
             else if (it == 0)
-                check_phase<true, CLAMP, DC>(plan, synm, total, c2b, row, n_tasks, n_pad, thr, wave, lane);
+                check_phase<kSrcFirst, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
+                                                  thr, wave, lane);
+            else if (it == 1 && MODE == kModeKeys && a.tab2_entries)
+                check_phase<kSrcTable, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
+                                                  thr, wave, lane);
             else
-                check_phase<false, CLAMP, DC>(plan, synm, total, c2b, row, n_tasks, n_pad, thr, wave, lane);
+                check_phase<kSrcGeneral, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
+                                                    thr, wave, lane);
             __syncthreads();
             pc.mark(1);
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
@@ -387,6 +461,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[k] : acc;
                     for (int k = kDvUnroll; k < deg; ++k) acc = acc + c2b[k * n_pad + i];
                     total[i] = acc;
+                    if (MODE == kModeKeys && a.tab2_entries && it == 0) {
+                        // second_table_index: bob bit and the signs of the first messages
+                        uint32_t code = (bobmask >> r) & 1u;
+#pragma unroll
+                        for (int k = 0; k < kTab2MaxDv; ++k)
+                            if (k < deg) code |= ((uint32_t)qkdm::hi32(v[k]) >> 31) << (1 + k);
+                        t2idx[i] = (uint16_t)(c.bit_pat[i] * tab2_stride(c.max_dv) + code * c.max_dv);
+                    }
                     if (acc <= 0.0) {
                         for (int k = 0; k < deg; ++k) {
                             const int j = c.bit_chk[k * n_pad + i];
@@ -556,7 +638,9 @@ static DecodeFn pick_decode(int mode, bool clamp, int max_dc, int* dc) {
     return clamp ? pick_decode_dc<kModeKeys, true>(max_dc, dc) : pick_decode_dc<kModeKeys, false>(max_dc, dc);
 }
 
-static size_t decode_lds_bytes(const qkd_code* c, int dc) { return DecodeLds(c->n_pad, c->n_tasks, c->m, dc).bytes; }
+static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries) {
+    return DecodeLds(c->n_pad, c->n_tasks, c->m, dc, tab2_entries).bytes;
+}
 
 // Resident workgroups of decode_kernel for this code on its device.
 static qkd_status decode_grid(const qkd_code* c, DecodeFn fn, size_t lds, int* grid) {
@@ -648,7 +732,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                                 hipStream_t stream) {
     int dc = 0;
     DecodeFn fn = pick_decode(mode, a.clamp_on != 0, c->max_dc, &dc);
-    const size_t lds = decode_lds_bytes(c, dc);
+    const size_t lds = decode_lds_bytes(c, dc, a.tab2_entries);
     int grid = 0;
     qkd_status s = decode_grid(c, fn, lds, &grid);
     if (s != QKD_OK) return s;
@@ -782,6 +866,7 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
             a.first_c2b[d] = v;
         }
     }
+    a.tab2_entries = (a.first_table && c->n_pat > 0) ? c->n_pat * tab2_stride(c->max_dv) : 0;
     a.bits_out = bits_out;
     a.iters = iters;
     a.sp_ok = sp_ok;

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <new>
 #include <sstream>
 
@@ -39,6 +40,10 @@ static void free_device(qkd_code* c) {
     if (c->d_chk_deg) (void)hipFree(c->d_chk_deg);
     if (c->d_bit_chk) (void)hipFree(c->d_bit_chk);
     if (c->d_bit_deg) (void)hipFree(c->d_bit_deg);
+    if (c->d_bit_pat) (void)hipFree(c->d_bit_pat);
+    if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
+    c->d_bit_pat = nullptr;
+    c->d_pat_deg = nullptr;
     if (c->d_plan) (void)hipFree(c->d_plan);
     if (c->d_plan_chk) (void)hipFree(c->d_plan_chk);
     c->d_plan = nullptr;
@@ -123,6 +128,31 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     if (!qkdp::build_wave_plan(n, m, cptr, cidx, krow.data(), plan))
         return set_error(QKD_ERR_UNSUPPORTED, "check degree outside [1, %d]", qkdp::kPlanMaxDegree);
     c->n_tasks = plan.n_tasks;
+    // degree patterns of the bits: the ascending checks' degrees
+    std::vector<uint16_t> bit_pat(n, 0);
+    c->n_pat = 0;
+    c->pat_deg.clear();
+    if (max_dv <= kTab2MaxDv) {
+        std::map<std::vector<uint8_t>, int> ids;
+        for (int32_t i = 0; i < n; ++i) {
+            std::vector<uint8_t> key(max_dv, 0);
+            for (int32_t k = c->bit_ptr[i]; k < c->bit_ptr[i + 1]; ++k) {
+                const int32_t j = c->bit_idx[k];
+                key[k - c->bit_ptr[i]] = (uint8_t)(cptr[j + 1] - cptr[j]);
+            }
+            auto it = ids.find(key);
+            if (it == ids.end()) {
+                it = ids.emplace(key, (int)ids.size()).first;
+                c->pat_deg.insert(c->pat_deg.end(), key.begin(), key.end());
+            }
+            bit_pat[i] = (uint16_t)it->second;
+        }
+        c->n_pat = (int32_t)ids.size();
+        if ((size_t)c->n_pat * tab2_stride(max_dv) > (size_t)kTab2MaxEntries) {
+            c->n_pat = 0;
+            c->pat_deg.clear();
+        }
+    }
     bool reg = true;
     for (int32_t i = 0; i < n; ++i) {
         bit_deg[i] = (uint8_t)bdeg[i];
@@ -148,6 +178,13 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     QKD_HIP(hipMemcpy(c->d_bit_chk, bit_chk.data(), bit_chk.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_bit_deg, bit_deg.data(), bit_deg.size(), hipMemcpyHostToDevice));
+    if (c->n_pat > 0) {
+        QKD_HIP(hipMalloc(&c->d_bit_pat, bit_pat.size() * sizeof(uint16_t)));
+        QKD_HIP(hipMalloc(&c->d_pat_deg, c->pat_deg.size()));
+        QKD_HIP(hipMemcpy(c->d_bit_pat, bit_pat.data(), bit_pat.size() * sizeof(uint16_t),
+                          hipMemcpyHostToDevice));
+        QKD_HIP(hipMemcpy(c->d_pat_deg, c->pat_deg.data(), c->pat_deg.size(), hipMemcpyHostToDevice));
+    }
     QKD_HIP(hipMalloc(&c->d_plan, plan.word.size() * sizeof(uint32_t)));
     QKD_HIP(hipMalloc(&c->d_plan_chk, plan.chk.size() * sizeof(int32_t)));
     QKD_HIP(hipMemcpy(c->d_plan, plan.word.data(), plan.word.size() * sizeof(uint32_t),

@@ -14,6 +14,13 @@ namespace qkd {
 
 // Threads per decode workgroup: one workgroup decodes one frame at a time.
 constexpr int kDecodeBlock = 1024;
+// Second-iteration tanh table (decode.hip): entries per degree pattern are
+// 2^(1 + max_dv) sign codes x max_dv rows; the table is used when
+// max_dv <= kTab2MaxDv and n_pat * entries <= kTab2MaxEntries.
+constexpr int kTab2MaxDv = 4;
+constexpr int kTab2MaxEntries = 2048;
+__host__ __device__ inline int tab2_stride(int max_dv) { return (1 << (1 + max_dv)) * max_dv; }
+
 // Largest check degree: one check's edges fit one wavefront (qkd_plan.h).
 constexpr int kMaxCheckDegree = 64;
 // The per-frame bit totals live in LDS as binary64: N <= this.
@@ -40,6 +47,12 @@ struct DeviceCode {
     const int32_t* plan_chk;
     const int32_t* bit_chk;
     const uint8_t* bit_deg;
+    // degree patterns of the bits (second-iteration tanh table, decode.hip):
+    // bit_pat[i] = pattern of bit i; pat_deg[p * max_dv + k] = degree of the
+    // k-th check of pattern p (0 past the bit's degree)
+    int32_t n_pat;
+    const uint16_t* bit_pat;
+    const uint8_t* pat_deg;
 };
 
 }  // namespace qkd
@@ -76,12 +89,17 @@ struct qkd_code {
     uint8_t* d_bit_deg = nullptr;
     uint32_t* d_plan = nullptr;
     int32_t* d_plan_chk = nullptr;
+    int32_t n_pat = 0;                  // 0: too many degree patterns for the table
+    std::vector<uint8_t> pat_deg;
+    uint16_t* d_bit_pat = nullptr;
+    uint8_t* d_pat_deg = nullptr;
     int cu_count = 0;
     qkd_workspace* default_ws = nullptr;
 
     qkd::DeviceCode view() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, n_tasks,
-                               d_chk_bits, d_chk_deg, d_plan, d_plan_chk, d_bit_chk, d_bit_deg};
+                               d_chk_bits, d_chk_deg, d_plan, d_plan_chk, d_bit_chk, d_bit_deg,
+                               n_pat, d_bit_pat, d_pat_deg};
     }
 };
 

@@ -299,18 +299,18 @@ QKD_HD double expm1_tanh_domain(double x) {
     const double Q5 = -2.01099218183624371326e-07;
 
     const uint32_t ahx = (uint32_t)hi32(x) & 0x7fffffffu;
-    const bool neg = x < 0.0;
     const bool red = ahx > 0x3fd62e42u;          // |x| > ln2/2: reduce
     const bool km1 = ahx < 0x3FF0A2B2u;          // |x| < 1.5 ln2 (negative side only here)
-    // general k = (int)(invln2*x -+ 0.5), hi = x - k*ln2_hi, lo = k*ln2_lo
-    const int kg = (int)(invln2 * x + (neg ? -0.5 : 0.5));
-    const double tg = (double)kg;
-    const double hi_g = x - tg * ln2_hi;
-    const double lo_g = tg * ln2_lo;
-    const double hi = red ? (km1 ? x + ln2_hi : hi_g) : x;
-    const double lo = red ? (km1 ? -ln2_lo : lo_g) : 0.0;
+    // general k = (int)(invln2*x -+ 0.5)
+    const int kg = (int)(invln2 * x + __builtin_copysign(0.5, x));
     const int k = red ? (km1 ? -1 : kg) : 0;
-    const double xr = hi - lo;                   // == x when k == 0
+    // The reference's three reductions are one formula in t = (double)k:
+    //   k = -1: hi = x + ln2_hi = x - (-1.0)*ln2_hi, lo = -ln2_lo = (-1.0)*ln2_lo
+    //   k =  0: hi = x - 0.0 = x (also for -0), lo = +0, so xr = x and c = 0
+    const double tk = (double)k;
+    const double hi = x - tk * ln2_hi;
+    const double lo = tk * ln2_lo;
+    const double xr = hi - lo;
     const double c = (hi - xr) - lo;
 
     const double hfx = 0.5 * xr;
@@ -328,10 +328,11 @@ QKD_HD double expm1_tanh_domain(double x) {
     const double e2 = (xr * (e - c) - c) - hxs;              // k != 0
     const double resm1 = 0.5 * (xr - e2) - 0.5;              // k == -1
     const bool big = k <= -2 || k > 56;
-    const int ks = k < 0 ? 0 : (k > 31 ? 31 : k);
-    const double t1 = from_bits((uint64_t)(0x3ff00000u - (0x200000u >> ks)) << 32);      // 1 - 2^-k
+    const int ks = (big || k > 31) ? 31 : (k < 0 ? 0 : k);
+    // 1 - 2^-k for 2 <= k < 20; exactly 1.0 when big (the shift leaves 0)
+    const double t1 = from_bits((uint64_t)(0x3ff00000u - (0x200000u >> ks)) << 32);
     const double t2 = from_bits((uint64_t)((uint32_t)(0x3ff - k) << 20) << 32);          // 2^-k
-    const double a12 = (big ? 1.0 : t1) - (e2 - xr);         // k <= -2 | k > 56 | 2 <= k < 20
+    const double a12 = t1 - (e2 - xr);                       // k <= -2 | k > 56 | 2 <= k < 20
     const double a3 = (xr - (e2 + t2)) + 1.0;                // 20 <= k <= 56
     const double a = (big || k < 20) ? a12 : a3;
     const double y = set_hi32(a, (uint32_t)hi32(a) + ((uint32_t)k << 20));

@@ -252,3 +252,44 @@ def test_alist_reader_roundtrip(Q, golden_code, tmp_path):
     assert (cp == g["chk_off"]).all() and (ci == g["chk_idx"]).all()
     assert (bp == g["bit_off"]).all() and (bi == g["bit_idx"]).all()
     assert not H.is_regular and H.max_bit_nodes_weight == 3 and H.max_check_nodes_weight == 6
+
+
+# ---- QKD path (keys mode): first-iteration and second-iteration tables -----------------
+
+def _qkd_both(Q, H, oc, alice, bob, q, max_it, thr, thr_on):
+    r = Q.qkd_ldpc(H, dev(alice, np.uint8), dev(bob, np.uint8), q, max_it, thr, thr_on,
+                   want_bits=True)
+    torch.cuda.synchronize()
+    its = r.iterations.cpu().numpy()
+    sp = r.syndromes_match.cpu().numpy()
+    ko = r.keys_match.cpu().numpy()
+    bits = r.bits.cpu().numpy()
+    for f in range(alice.shape[0]):
+        want = oc.qkd_ldpc(alice[f], bob[f], q, max_it, thr, thr_on)
+        assert its[f] == want["iters"], (q, thr, thr_on, max_it, f)
+        assert bool(sp[f]) == want["sp_ok"] and bool(ko[f]) == want["key_ok"]
+        assert (bits[f] == want["out"]).all(), (q, thr, thr_on, max_it, f)
+
+
+@pytest.mark.parametrize("q", [0.02, 0.08, 0.11, 0.5, 0.7])
+@pytest.mark.parametrize("thr,thr_on", [(100.0, True), (2.5, True), (0.7, True), (100.0, False)])
+def test_qkd_ldpc_tables_bits_match_oracle(Q, H, oracle_code, oracle_mod, q, thr, thr_on):
+    """The QKD path replaces the first check phase by a sign/degree table and the
+    second iteration's tanh by a lookup; decoded words, iteration counts and flags
+    must still equal the oracle's bit for bit, including failing frames (q >= 0.11),
+    log((1-q)/q) = 0 (q = 0.5: NaN messages) and negative LLR magnitudes (q > 0.5)."""
+    rng = np.random.default_rng(int(q * 1000) + int(thr * 10) + thr_on)
+    f = 3
+    alice = rng.integers(0, 2, (f, 10240))
+    flips = rng.random((f, 10240)) < min(q, 0.3)
+    bob = alice ^ flips
+    max_it = 12 if q >= 0.11 else 50
+    _qkd_both(Q, H, oracle_code, alice, bob, q, max_it, thr, thr_on)
+
+
+@pytest.mark.parametrize("max_it", [1, 2, 3])
+def test_qkd_ldpc_iteration_caps_inside_tables(Q, H, oracle_code, max_it):
+    rng = np.random.default_rng(max_it)
+    alice = rng.integers(0, 2, (4, 10240))
+    bob = alice ^ (rng.random((4, 10240)) < 0.05)
+    _qkd_both(Q, H, oracle_code, alice, bob, 0.05, max_it, 100.0, True)
