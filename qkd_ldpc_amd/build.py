@@ -20,6 +20,8 @@ def build(clean: bool = False, jobs: int = 4) -> str:
     if clean:
         subprocess.check_call(["make", "-C", CSRC, "clean"], env=env)
     subprocess.check_call(["make", "-s", "-C", CSRC, f"-j{jobs}"], env=env)
+    # the reference-signature C++ shim (compat/) on top of the C ABI
+    subprocess.check_call(["make", "-s", "-C", os.path.join(os.path.dirname(HERE), "compat")], env=env)
     return os.path.join(HERE, "lib", "libqkd_ldpc_amd.so")
 
 
