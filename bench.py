@@ -213,9 +213,9 @@ def main():
             },
         }
         if os.environ.get("QKD_PHASE_TIMING"):
-            cyc = np.zeros(5, np.uint64)
+            cyc = np.zeros(7, np.uint64)
             Q._native.check(L.qkd_debug_phase_cycles(ws.handle, cyc.ctypes.data))
-            names = ["prologue", "check", "bit", "syndrome", "fetch_out"]
+            names = ["prologue", "check", "bit", "syndrome", "fetch_out", "check_first", "check_second"]
             tot = float(cyc.sum()) or 1.0
             out["phase_share"] = {n: float(v) / tot for n, v in zip(names, cyc)}
         if world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:

@@ -177,10 +177,11 @@ QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t 
  * With QKD_PHASE_TIMING set in the environment, decode launches on `ws`
  * accumulate shader-clock cycles per phase, summed over workgroups (thread 0
  * between barriers): [0] per-frame prologue, [1] check phase, [2] bit phase,
- * [3] syndrome test, [4] frame fetch + outputs. Synchronises the device. No
+ * [3] syndrome test, [4] frame fetch + outputs, [5] / [6] the table-driven
+ * first / second check phases of the QKD path. Synchronises the device. No
  * reference counterpart (the reference prints TRACE_* arrays instead,
  * qkd_ldpc_algorithm.cpp:42-155). */
-QKD_API qkd_status qkd_debug_phase_cycles(qkd_workspace *ws, uint64_t *cycles5);
+QKD_API qkd_status qkd_debug_phase_cycles(qkd_workspace *ws, uint64_t *cycles7);
 
 /* ---- host helpers --------------------------------------------------------- */
 /* seeds[k] = k-th raw xoshiro256++(simulation_seed) output (simulation.cpp:222-228). */

@@ -85,7 +85,7 @@ struct DecodeArgs {
 // Phase-clock accumulation (diagnostic; a wave-uniform test when off).
 struct PhaseClock {
     unsigned long long* out;
-    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
     long long t = 0;
     __device__ explicit PhaseClock(unsigned long long* o) : out(threadIdx.x == 0 ? o : nullptr) {
         if (out) t = clock64();
@@ -99,7 +99,7 @@ struct PhaseClock {
     }
     __device__ void flush() {
         if (out)
-            for (int k = 0; k < 5; ++k) atomicAdd(out + k, acc[k]);
+            for (int k = 0; k < 7; ++k) atomicAdd(out + k, acc[k]);
     }
 };
 
@@ -129,6 +129,7 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) 
 //   tsyn   [m_words]        target syndrome, one bit per check
 //   xsyn   [m_words]        syndrome of the current hard decision (XOR-built)
 //   tval   [NW][64 + DC]    per-wave tanh values for the in-check products
+//                           (prologue: staged syndrome bytes / Alice words)
 //   ctab   [kFirstTableDeg+1] first-iteration message magnitudes by degree
 //   tab2   [tab2_entries]   second-iteration tanh table
 //   t2idx  [n_pad]          per-bit base index into tab2 (uint16)
@@ -141,7 +142,11 @@ struct DecodeLds {
         tsyn = synm + (size_t)n_tasks * 8;
         xsyn = tsyn + (size_t)m_words * 4;
         tval = (xsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
-        ctab = tval + (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
+        // the tanh rows double as the prologue's staging area (syndrome bytes
+        // or Alice's words), so the region is at least that large
+        const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
+        const size_t stage = (size_t)m > (size_t)(n_pad / 64 + 1) * 8 ? (size_t)m : (size_t)(n_pad / 64 + 1) * 8;
+        ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         t2idx = tab2 + (size_t)tab2_entries * 8;
         ctl = (t2idx + (tab2_entries ? (size_t)n_pad * 2 : 0) + 15) & ~(size_t)15;
@@ -149,8 +154,13 @@ struct DecodeLds {
     }
 };
 
-// Bit-phase loads issued together before the ordered sum.
+// Bit phase: message rows per bit loaded ahead of the ordered sum, and rounds
+// (bits tid + r*kDecodeBlock) per load batch.
 constexpr int kDvUnroll = 4;
+constexpr int kBitChunk = 4;
+// Plan-walking loops outside the check phase load this many tasks' plan words
+// per trip (the plan carries kPlanPadTasks >= kPlanGroup * NW idle tasks).
+constexpr int kPlanGroup = 4;
 
 // ---- wave-plan words (qkd_plan.h) ------------------------------------------
 __device__ __forceinline__ uint32_t pw_bit(uint32_t w) { return w & qkdp::kPlanBitMask; }
@@ -316,13 +326,22 @@ __device__ __forceinline__ void first_check_phase(const uint32_t* __restrict__ p
                                                   double* __restrict__ c2b, int n_tasks, int n_pad, int wave,
                                                   int lane) {
     constexpr int NW = kDecodeBlock / 64;
-    for (int t = wave; t < n_tasks; t += NW) {
-        const uint32_t w = plan[t * 64 + lane];
-        const uint32_t bit = pw_bit(w);
-        const uint32_t sg = (uint32_t)qkdm::hi32(total[bit]) >> 31;
-        const uint32_t sp = (uint32_t)((synm[t] >> lane) & 1ull) ^ (uint32_t)seg_parity(__ballot(sg), w);
-        const double cm = ctab[pw_deg(w)];
-        c2b[pw_row(w) * n_pad + bit] = (sp ^ sg) ? -cm : cm;
+    // kPlanGroup tasks per trip: their plan words are loaded together (the
+    // plan is padded, so the loads need no bounds test); stores are predicated.
+    for (int t0 = wave; t0 < n_tasks; t0 += NW * kPlanGroup) {
+        uint32_t w[kPlanGroup];
+#pragma unroll
+        for (int u = 0; u < kPlanGroup; ++u) w[u] = plan[(t0 + u * NW) * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < kPlanGroup; ++u) {
+            const int t = t0 + u * NW;
+            if (t >= n_tasks) break;
+            const uint32_t bit = pw_bit(w[u]);
+            const uint32_t sg = (uint32_t)qkdm::hi32(total[bit]) >> 31;
+            const uint32_t sp = (uint32_t)((synm[t] >> lane) & 1ull) ^ (uint32_t)seg_parity(__ballot(sg), w[u]);
+            const double cm = ctab[pw_deg(w[u])];
+            c2b[pw_row(w[u]) * n_pad + bit] = (sp ^ sg) ? -cm : cm;
+        }
     }
 }
 
@@ -332,7 +351,11 @@ __device__ __forceinline__ void first_check_phase(const uint32_t* __restrict__ p
 //
 // Message store: the c2b messages of the frame live bit-major in global memory,
 // c2b[k * n_pad + i] = message from the k-th check (ascending) of bit i, i.e.
-// the reference's c2b[i][k] layout transposed for coalescing (:192-205).
+// the reference's c2b[i][k] layout transposed for coalescing (:192-205). The
+// check phase's gather/scatter of it overlaps its transcendental arithmetic;
+// the bit phase streams it. (A plan-order store, coalesced in the check phase
+// and gathered in the bit phase, measured 10 % slower overall: the gathers
+// then stall a phase with nothing to overlap.)
 //
 // Per iteration:
 //  check phase (check_phase above), one edge per lane, wave tasks of whole
@@ -405,24 +428,48 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             }
             if (tid == 0) total[c.n] = 0.0;
         }
-        // ---- prologue: target syndrome, per wave task and per check
-        for (int t = wave; t < n_tasks; t += NW) {
-            const int slot = t * 64 + lane;
-            const uint32_t w = plan[slot];
-            const int j = c.plan_chk[slot];
-            int s;
+        // ---- prologue: target syndrome, per wave task and per check. The
+        //      frame's Alice words (or syndrome bytes) are staged in LDS (the
+        //      tanh rows are free until the first check phase), so each task
+        //      needs only its two coalesced plan loads.
+        {
+            uint8_t* stage = reinterpret_cast<uint8_t*>(smem + L.tval);
             if (MODE == kModeLlr) {
-                s = j >= 0 ? (a.syn[(size_t)f * c.m + j] != 0) : 0;
+                for (int j = tid; j < c.m; j += kDecodeBlock) stage[j] = a.syn[(size_t)f * c.m + j] != 0;
             } else {
-                // calculate_syndrome_irregular on Alice's key (:413-414)
-                const uint32_t bit = pw_bit(w);
-                int ab = 0;
-                if (j >= 0) ab = (int)((a.alice_w[(size_t)f * a.words + (bit >> 6)] >> (bit & 63)) & 1u);
-                s = seg_parity(__ballot(ab), w);
+                uint64_t* sw = reinterpret_cast<uint64_t*>(stage);
+                for (int w = tid; w < (int)a.words; w += kDecodeBlock) sw[w] = a.alice_w[(size_t)f * a.words + w];
             }
-            const uint64_t sm = __ballot(s);
-            if (lane == 0) synm[t] = sm;
-            if (s && j >= 0 && lane == pw_start(w)) atomicOr(&tsyn[j >> 5], 1u << (j & 31));
+            __syncthreads();
+            for (int t0 = wave; t0 < n_tasks; t0 += NW * kPlanGroup) {
+                uint32_t wg[kPlanGroup];
+                int jg[kPlanGroup];
+#pragma unroll
+                for (int u = 0; u < kPlanGroup; ++u) {
+                    wg[u] = plan[(t0 + u * NW) * 64 + lane];
+                    jg[u] = c.plan_chk[(t0 + u * NW) * 64 + lane];
+                }
+#pragma unroll
+                for (int u = 0; u < kPlanGroup; ++u) {
+                const int t = t0 + u * NW;
+                if (t >= n_tasks) break;
+                const uint32_t w = wg[u];
+                const int j = jg[u];
+                int s;
+                if (MODE == kModeLlr) {
+                    s = j >= 0 ? stage[j] : 0;
+                } else {
+                    // calculate_syndrome_irregular on Alice's key (:413-414)
+                    const uint32_t bit = pw_bit(w);
+                    const uint64_t* sw = reinterpret_cast<const uint64_t*>(stage);
+                    const int ab = j >= 0 ? (int)((sw[bit >> 6] >> (bit & 63)) & 1u) : 0;
+                    s = seg_parity(__ballot(ab), w);
+                }
+                const uint64_t sm = __ballot(s);
+                if (lane == 0) synm[t] = sm;
+                if (s && j >= 0 && lane == pw_start(w)) atomicOr(&tsyn[j >> 5], 1u << (j & 31));
+                }
+            }
         }
         __syncthreads();
         pc.mark(0);
@@ -443,22 +490,38 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                 check_phase<kSrcGeneral, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
                                                     thr, wave, lane);
             __syncthreads();
-            pc.mark(1);
+            pc.mark((MODE == kModeKeys && it < 2 && a.first_table) ? 5 + (int)it : 1);
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
-            // and the hard decision's syndrome (:277, calculate_syndrome_irregular :476-486)
-            {
-                int r = 0;
-#pragma unroll 2
-                for (int i = tid; i < c.n; i += kDecodeBlock, ++r) {
+            // and the hard decision's syndrome (:277, calculate_syndrome_irregular :476-486).
+            // kBitChunk rounds at a time: all their message rows and check indices
+            // are loaded before any of them is summed.
+            for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kBitChunk) {
+                double v[kBitChunk][kDvUnroll];
+                int32_t jc[kBitChunk][kDvUnroll];
+                int dg[kBitChunk];
+#pragma unroll
+                for (int u = 0; u < kBitChunk; ++u) {
+                    const int i = tid + (r0 + u) * kDecodeBlock;
+                    const bool ok = i < c.n;
+                    dg[u] = ok ? c.bit_deg[i] : 0;
+#pragma unroll
+                    for (int k = 0; k < kDvUnroll; ++k) {
+                        const bool ld = ok && k < c.max_dv;
+                        v[u][k] = ld ? c2b[k * n_pad + i] : 0.0;
+                        jc[u][k] = ld ? c.bit_chk[k * n_pad + i] : 0;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kBitChunk; ++u) {
+                    const int r = r0 + u;
+                    const int i = tid + r * kDecodeBlock;
+                    if (i >= c.n) break;
+                    const int deg = dg[u];
                     double acc;
                     if (MODE == kModeLlr) acc = a.llr[(size_t)f * c.n + i];
                     else acc = ((bobmask >> r) & 1u) ? -a.log_p : a.log_p;
-                    const int deg = c.bit_deg[i];
-                    double v[kDvUnroll];
 #pragma unroll
-                    for (int k = 0; k < kDvUnroll; ++k) v[k] = k < c.max_dv ? c2b[k * n_pad + i] : 0.0;
-#pragma unroll
-                    for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[k] : acc;
+                    for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
                     for (int k = kDvUnroll; k < deg; ++k) acc = acc + c2b[k * n_pad + i];
                     total[i] = acc;
                     if (MODE == kModeKeys && a.tab2_entries && it == 0) {
@@ -466,11 +529,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                         uint32_t code = (bobmask >> r) & 1u;
 #pragma unroll
                         for (int k = 0; k < kTab2MaxDv; ++k)
-                            if (k < deg) code |= ((uint32_t)qkdm::hi32(v[k]) >> 31) << (1 + k);
+                            if (k < deg) code |= ((uint32_t)qkdm::hi32(v[u][k]) >> 31) << (1 + k);
                         t2idx[i] = (uint16_t)(c.bit_pat[i] * tab2_stride(c.max_dv) + code * c.max_dv);
                     }
                     if (acc <= 0.0) {
-                        for (int k = 0; k < deg; ++k) {
+#pragma unroll
+                        for (int k = 0; k < kDvUnroll; ++k)
+                            if (k < deg) atomicXor(&xsyn[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
+                        for (int k = kDvUnroll; k < deg; ++k) {
                             const int j = c.bit_chk[k * n_pad + i];
                             atomicXor(&xsyn[j >> 5], 1u << (j & 31));
                         }
@@ -530,16 +596,17 @@ __global__ void syndrome_kernel(DeviceCode c, const uint8_t* bits, uint32_t n_fr
 }
 
 // ---- bit packing ------------------------------------------------------------
+// One lane per bit, one wave per 64-bit word: coalesced byte reads, one ballot.
 __global__ void pack_kernel(const uint8_t* bytes, uint32_t n, uint32_t words, uint32_t n_frames,
                             uint64_t* out) {
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (size_t)n_frames * words) return;
-    const size_t f = gid / words;
-    const uint32_t w = (uint32_t)(gid - f * words);
-    uint64_t v = 0;
-    const uint32_t lo = w * 64, hi = min(n, lo + 64);
-    for (uint32_t i = lo; i < hi; ++i) v |= (uint64_t)(bytes[f * n + i] & 1u) << (i - lo);
-    out[gid] = v;
+    const size_t word = gid >> 6;                     // wave-uniform
+    if (word >= (size_t)n_frames * words) return;
+    const size_t f = word / words;
+    const uint32_t i = (uint32_t)(word - f * words) * 64 + (threadIdx.x & 63);
+    const int b = i < n ? (bytes[f * n + i] & 1) : 0;
+    const uint64_t v = __ballot(b);
+    if ((threadIdx.x & 63) == 0) out[word] = v;
 }
 
 __global__ void unpack_kernel(const uint64_t* words_in, uint32_t n, uint32_t words, uint32_t n_frames,
@@ -894,9 +961,9 @@ qkd_status qkd_qkd_ldpc_batch(const qkd_code* c, qkd_workspace* ws, const uint8_
     if (s != QKD_OK) return s;
     const uint32_t words = (uint32_t)((c->n + 63) / 64);
     const size_t nw = n_frames * words;
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw, 256)), dim3(256), 0, (hipStream_t)stream, alice,
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 64, 256)), dim3(256), 0, (hipStream_t)stream, alice,
                        (uint32_t)c->n, words, (uint32_t)n_frames, ws->alice_w);
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw, 256)), dim3(256), 0, (hipStream_t)stream, bob,
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 64, 256)), dim3(256), 0, (hipStream_t)stream, bob,
                        (uint32_t)c->n, words, (uint32_t)n_frames, ws->bob_w);
     QKD_HIP(hipGetLastError());
     return decode_keys(c, ws, n_frames, qber, max_iterations, msg_threshold, flags, bits_out, iterations,
@@ -943,12 +1010,12 @@ qkd_status qkd_keygen_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t
     return QKD_OK;
 }
 
-qkd_status qkd_debug_phase_cycles(qkd_workspace* ws, uint64_t* cycles5) {
-    if (!ws || !cycles5) return set_error(QKD_ERR_INVALID_ARG, "null argument");
+qkd_status qkd_debug_phase_cycles(qkd_workspace* ws, uint64_t* cycles7) {
+    if (!ws || !cycles7) return set_error(QKD_ERR_INVALID_ARG, "null argument");
     if (!ws->counter) return set_error(QKD_ERR_INVALID_ARG, "workspace has not decoded yet");
     DeviceGuard g(ws->device);
     QKD_HIP(hipDeviceSynchronize());
-    QKD_HIP(hipMemcpy(cycles5, reinterpret_cast<char*>(ws->counter) + 64, 40, hipMemcpyDeviceToHost));
+    QKD_HIP(hipMemcpy(cycles7, reinterpret_cast<char*>(ws->counter) + 64, 56, hipMemcpyDeviceToHost));
     return QKD_OK;
 }
 

@@ -39,6 +39,8 @@ static void free_device(qkd_code* c) {
     if (c->d_chk_bits) (void)hipFree(c->d_chk_bits);
     if (c->d_chk_deg) (void)hipFree(c->d_chk_deg);
     if (c->d_bit_chk) (void)hipFree(c->d_bit_chk);
+    if (c->d_bit_slot) (void)hipFree(c->d_bit_slot);
+    c->d_bit_slot = nullptr;
     if (c->d_bit_deg) (void)hipFree(c->d_bit_deg);
     if (c->d_bit_pat) (void)hipFree(c->d_bit_pat);
     if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
@@ -128,6 +130,16 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     if (!qkdp::build_wave_plan(n, m, cptr, cidx, krow.data(), plan))
         return set_error(QKD_ERR_UNSUPPORTED, "check degree outside [1, %d]", qkdp::kPlanMaxDegree);
     c->n_tasks = plan.n_tasks;
+    std::vector<int32_t> bit_slot((size_t)max_dv * c->n_pad, 0);
+    {
+        std::vector<int32_t> fill2(c->bit_ptr.begin(), c->bit_ptr.end() - 1);
+        for (int32_t j = 0; j < m; ++j)
+            for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) {
+                const int32_t b = cidx[k];
+                const int32_t bk = fill2[b]++ - c->bit_ptr[b];
+                bit_slot[(size_t)bk * c->n_pad + b] = plan.slot_of_edge[k];
+            }
+    }
     // degree patterns of the bits: the ascending checks' degrees
     std::vector<uint16_t> bit_pat(n, 0);
     c->n_pat = 0;
@@ -175,6 +187,8 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     QKD_HIP(hipMemcpy(c->d_chk_bits, chk_bits.data(), chk_bits.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_chk_deg, chk_deg.data(), chk_deg.size(), hipMemcpyHostToDevice));
+    QKD_HIP(hipMalloc(&c->d_bit_slot, bit_slot.size() * sizeof(int32_t)));
+    QKD_HIP(hipMemcpy(c->d_bit_slot, bit_slot.data(), bit_slot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_bit_chk, bit_chk.data(), bit_chk.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_bit_deg, bit_deg.data(), bit_deg.size(), hipMemcpyHostToDevice));

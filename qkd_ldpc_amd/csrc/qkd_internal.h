@@ -31,9 +31,9 @@ constexpr int kMaxBitsLds = 20480;
 //                            (thread-per-check syndrome kernel)
 //   plan[s], plan_chk[s]     the check-phase wave plan (qkd_plan.h): slot
 //                            s = task*64 + lane holds one edge
-//   bit_chk[k * n_pad + i]   k-th check of bit i (ascending), -1 pad; c2b
-//                            messages are stored per frame bit-major in the
-//                            same [k][i] shape
+//   bit_chk[k * n_pad + i]   k-th check of bit i (ascending), -1 pad
+//   bit_slot[k * n_pad + i]  plan slot of that edge (c2b messages are stored
+//                            per frame in plan order)
 // Slot-major ("ELL") layouts keep lane-consecutive bits on consecutive
 // addresses.
 struct DeviceCode {
@@ -46,6 +46,7 @@ struct DeviceCode {
     const uint32_t* plan;
     const int32_t* plan_chk;
     const int32_t* bit_chk;
+    const int32_t* bit_slot;
     const uint8_t* bit_deg;
     // degree patterns of the bits (second-iteration tanh table, decode.hip):
     // bit_pat[i] = pattern of bit i; pat_deg[p * max_dv + k] = degree of the
@@ -86,6 +87,7 @@ struct qkd_code {
     int32_t* d_chk_bits = nullptr;
     uint8_t* d_chk_deg = nullptr;
     int32_t* d_bit_chk = nullptr;
+    int32_t* d_bit_slot = nullptr;
     uint8_t* d_bit_deg = nullptr;
     uint32_t* d_plan = nullptr;
     int32_t* d_plan_chk = nullptr;
@@ -98,7 +100,7 @@ struct qkd_code {
 
     qkd::DeviceCode view() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, n_tasks,
-                               d_chk_bits, d_chk_deg, d_plan, d_plan_chk, d_bit_chk, d_bit_deg,
+                               d_chk_bits, d_chk_deg, d_plan, d_plan_chk, d_bit_chk, d_bit_slot, d_bit_deg,
                                n_pat, d_bit_pat, d_pat_deg};
     }
 };
