@@ -128,24 +128,26 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) 
 //   synm   [n_tasks]        target syndrome per wave task, one bit per lane
 //   tsyn   [m_words]        target syndrome, one bit per check
 //   xsyn   [m_words]        syndrome of the current hard decision (XOR-built)
+//   qsyn   [m_words]        QKD path: sign of each check's first-iteration product
 //   tval   [NW][64 + DC]    per-wave tanh values for the in-check products
-//                           (prologue: staged syndrome bytes / Alice words)
+//                           (prologue: staged syndrome bytes / Alice+Bob words)
 //   ctab   [kFirstTableDeg+1] first-iteration message magnitudes by degree
 //   tab2   [tab2_entries]   second-iteration tanh table
 //   t2idx  [n_pad]          per-bit base index into tab2 (uint16)
 //   ctl    [4]              frame index, block_any flags
 struct DecodeLds {
-    size_t synm, tsyn, xsyn, tval, ctab, tab2, t2idx, ctl, bytes;
+    size_t synm, tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, bytes;
     __host__ __device__ DecodeLds(int n_pad, int n_tasks, int m, int dc, int tab2_entries) {
         const int m_words = (m + 31) / 32;
         synm = (size_t)n_pad * 8;
         tsyn = synm + (size_t)n_tasks * 8;
         xsyn = tsyn + (size_t)m_words * 4;
-        tval = (xsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
+        qsyn = xsyn + (size_t)m_words * 4;
+        tval = (qsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
         // the tanh rows double as the prologue's staging area (syndrome bytes
         // or Alice's words), so the region is at least that large
         const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
-        const size_t stage = (size_t)m > (size_t)(n_pad / 64 + 1) * 8 ? (size_t)m : (size_t)(n_pad / 64 + 1) * 8;
+        const size_t stage = (size_t)m > (size_t)(n_pad / 64 + 1) * 16 ? (size_t)m : (size_t)(n_pad / 64 + 1) * 16;
         ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         t2idx = tab2 + (size_t)tab2_entries * 8;
@@ -310,6 +312,12 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
     __syncthreads();
 }
 
+// fold_first_message: when the second table is also in use, nothing reads the
+// first iteration's stored messages (the second check phase takes its inputs
+// from the table), so the first check phase is skipped and the first bit phase
+// rebuilds each message from one sign bit per check (qsyn, the sign of P_j,
+// computed in the prologue from Bob's bits) and the bit's own LLR sign.
+//
 // First check phase of the QKD path (QKD_LDPC_irregular, :398-425 -> :220-249
 // at it = 0), where b2c = LLR_i = bob_i ? -log_p : +log_p for every edge. Then
 //   t_i = tanh(LLR_i / 2) = sign_i * T,  T = |tanh(log_p / 2)|  (tanh is odd)
@@ -376,6 +384,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     uint64_t* synm = reinterpret_cast<uint64_t*>(smem + L.synm);
     uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
+    uint32_t* qsyn = reinterpret_cast<uint32_t*>(smem + L.qsyn);
+    // QKD path with both tables: the first check phase is folded into the
+    // first bit phase (fold_first_message)
+    const bool fold1 = MODE == kModeKeys && a.first_table && a.tab2_entries;
+    const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;     // sign bit of log_p
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
     double* tab2 = reinterpret_cast<double*>(smem + L.tab2);
@@ -404,6 +417,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         for (int w = tid; w < m_words; w += kDecodeBlock) {
             tsyn[w] = 0;
             xsyn[w] = 0;
+            qsyn[w] = 0;
         }
         __syncthreads();
         const uint32_t f = ctl[0];
@@ -438,7 +452,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                 for (int j = tid; j < c.m; j += kDecodeBlock) stage[j] = a.syn[(size_t)f * c.m + j] != 0;
             } else {
                 uint64_t* sw = reinterpret_cast<uint64_t*>(stage);
-                for (int w = tid; w < (int)a.words; w += kDecodeBlock) sw[w] = a.alice_w[(size_t)f * a.words + w];
+                for (int w = tid; w < (int)a.words; w += kDecodeBlock) {
+                    sw[w] = a.alice_w[(size_t)f * a.words + w];
+                    sw[a.words + w] = a.bob_w[(size_t)f * a.words + w];
+                }
             }
             __syncthreads();
             for (int t0 = wave; t0 < n_tasks; t0 += NW * kPlanGroup) {
@@ -468,6 +485,15 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                 const uint64_t sm = __ballot(s);
                 if (lane == 0) synm[t] = sm;
                 if (s && j >= 0 && lane == pw_start(w)) atomicOr(&tsyn[j >> 5], 1u << (j & 31));
+                if (MODE == kModeKeys && fold1) {
+                    // sign of the first-iteration product P of check j: s_j ^ the
+                    // sign bits of its LLRs (bob_i ^ sign(log_p)), fold_first_message
+                    const uint32_t bit = pw_bit(w);
+                    const uint64_t* bw = reinterpret_cast<const uint64_t*>(stage) + a.words;
+                    const int sg = j >= 0 ? (int)(((bw[bit >> 6] >> (bit & 63)) & 1u) ^ lsign) : 0;
+                    const int qs = s ^ seg_parity(__ballot(sg), w);
+                    if (qs && j >= 0 && lane == pw_start(w)) atomicOr(&qsyn[j >> 5], 1u << (j & 31));
+                }
                 }
             }
         }
@@ -478,7 +504,9 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         bool done = false;
         uint32_t it = 0;
         for (; it < a.max_it; ++it) {
-            if (it == 0 && MODE == kModeKeys && a.first_table)
+            if (it == 0 && fold1)
+                ;   // messages rebuilt from signs in the bit phase (fold_first_message)
+            else if (it == 0 && MODE == kModeKeys && a.first_table)
                 first_check_phase(plan, synm, total, ctab, c2b, n_tasks, n_pad, wave, lane);
             else if (it == 0)
                 check_phase<kSrcFirst, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
@@ -507,7 +535,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k) {
                         const bool ld = ok && k < c.max_dv;
-                        v[u][k] = ld ? c2b[k * n_pad + i] : 0.0;
+                        v[u][k] = (ld && !(fold1 && it == 0)) ? c2b[k * n_pad + i] : 0.0;
                         jc[u][k] = ld ? c.bit_chk[k * n_pad + i] : 0;
                     }
                 }
@@ -520,6 +548,21 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     double acc;
                     if (MODE == kModeLlr) acc = a.llr[(size_t)f * c.n + i];
                     else acc = ((bobmask >> r) & 1u) ? -a.log_p : a.log_p;
+                    if (MODE == kModeKeys && fold1 && it == 0) {
+                        // fold_first_message: message of the k-th check j of bit i is
+                        // +-C_{d_j} with sign = sign(P_j) ^ sign(LLR_i) (first_check_phase)
+                        const uint32_t sgi = ((bobmask >> r) & 1u) ^ lsign;
+                        const uint8_t* pd = c.pat_deg + c.bit_pat[i] * c.max_dv;
+#pragma unroll
+                        for (int k = 0; k < kDvUnroll; ++k) {
+                            if (k < deg) {
+                                const int j = jc[u][k];
+                                const uint32_t sp = (qsyn[j >> 5] >> (j & 31)) & 1u;
+                                const double cm = ctab[pd[k]];
+                                v[u][k] = (sp ^ sgi) ? -cm : cm;
+                            }
+                        }
+                    }
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
                     for (int k = kDvUnroll; k < deg; ++k) acc = acc + c2b[k * n_pad + i];
