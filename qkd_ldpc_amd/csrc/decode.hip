@@ -192,12 +192,25 @@ enum CheckSrc : int {
 
 template <int SRC, bool CLAMP, int DC>
 __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, uint64_t sm, int lane,
-                                             double thr, double* row) {
+                                             double thr, double* row, int min_dc, uint32_t dummy) {
     if (SRC == kSrcGeneral) {
         x = x - old;
         if (CLAMP) x = clamp_msg(x, thr);
     }
-    const double tv = SRC == kSrcTable ? x : qkdm::tanh_flat(x / 2.0);
+    const double xh = x / 2.0;
+    // Saturated wave: every lane's |b2c/2| >= 22 (finite or inf, not NaN) or idle.
+    // Then tanh is exactly +-1 (tanh_flat's |x| >= 22 branch), the product is
+    // +-1, P/t = +-1 and 2*atanh(+-1) = +-inf, clamped to +-thr: the message is
+    // that value with the sign of P*t, bit for bit, without the transcendentals.
+    bool fast = false;
+    if (SRC == kSrcGeneral) {
+        const uint32_t ax = (uint32_t)qkdm::hi32(xh) & 0x7fffffffu;
+        const bool sat = (ax >= 0x40360000u && !(xh != xh)) || pw_bit(w) == dummy;
+        fast = __all(sat);
+    }
+    double tv;
+    if (fast) tv = __builtin_copysign(1.0, xh);
+    else tv = SRC == kSrcTable ? x : qkdm::tanh_flat(xh);
     row[lane] = tv;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -208,8 +221,17 @@ __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, u
 #pragma unroll
     for (int k = 0; k < DC; ++k) o[k] = row[start + k];
     double P = ((sm >> lane) & 1ull) ? -1.0 : 1.0;
+    // factors below the code's smallest check degree belong to every lane
 #pragma unroll
-    for (int k = 0; k < DC; ++k) P = k < deg ? P * o[k] : P;
+    for (int k = 0; k < DC; ++k) {
+        if (k < min_dc) P = P * o[k];
+        else P = k < deg ? P * o[k] : P;
+    }
+    if (fast) {
+        const double inf = __builtin_inf();
+        const double mag = CLAMP ? (inf > thr ? thr : inf) : inf;
+        return (P * tv) < 0.0 ? -mag : mag;      // P, tv are +-1: P/tv == P*tv
+    }
     double v = 2.0 * qkdm::atanh_flat(P / tv);
     if (CLAMP) v = clamp_msg(v, thr);
     return v;
@@ -229,7 +251,8 @@ template <int SRC, bool CLAMP, int DC>
 __device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, const uint64_t* synm,
                                             const double* total, const uint16_t* t2idx, const double* tab2,
                                             double* __restrict__ c2b, double* row,
-                                            int n_tasks, int n_pad, double thr, int wave, int lane) {
+                                            int n_tasks, int n_pad, double thr, int wave, int lane,
+                                            int min_dc, uint32_t dummy) {
     constexpr int NW = kDecodeBlock / 64;
     constexpr bool FIRST = SRC != kSrcGeneral;    // no stored message is read
     int t = wave;
@@ -251,7 +274,7 @@ __device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, c
         const uint32_t wc = pl[(t + 2 * NW) * 64];
         const double xb = src(wb);
         const double ob = FIRST ? 0.0 : *msg(wb);
-        pv = check_edge<SRC, CLAMP, DC>(xa, oa, wa, synm[t], lane, thr, row);
+        pv = check_edge<SRC, CLAMP, DC>(xa, oa, wa, synm[t], lane, thr, row, min_dc, dummy);
         pend = msg(wa);
         t += NW;
         if (t >= n_tasks) break;
@@ -259,7 +282,7 @@ __device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, c
         wa = pl[(t + 2 * NW) * 64];
         xa = src(wc);
         oa = FIRST ? 0.0 : *msg(wc);
-        pv = check_edge<SRC, CLAMP, DC>(xb, ob, wb, synm[t], lane, thr, row);
+        pv = check_edge<SRC, CLAMP, DC>(xb, ob, wb, synm[t], lane, thr, row, min_dc, dummy);
         pend = msg(wb);
         t += NW;
         if (t >= n_tasks) break;
@@ -510,13 +533,13 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                 first_check_phase(plan, synm, total, ctab, c2b, n_tasks, n_pad, wave, lane);
             else if (it == 0)
                 check_phase<kSrcFirst, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
-                                                  thr, wave, lane);
+                                                  thr, wave, lane, c.min_dc, (uint32_t)c.n);
             else if (it == 1 && MODE == kModeKeys && a.tab2_entries)
                 check_phase<kSrcTable, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
-                                                  thr, wave, lane);
+                                                  thr, wave, lane, c.min_dc, (uint32_t)c.n);
             else
                 check_phase<kSrcGeneral, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
-                                                    thr, wave, lane);
+                                                    thr, wave, lane, c.min_dc, (uint32_t)c.n);
             __syncthreads();
             pc.mark((MODE == kModeKeys && it < 2 && a.first_table) ? 5 + (int)it : 1);
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),

@@ -99,6 +99,8 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     c->m = m;
     c->e = e;
     c->max_dc = max_dc;
+    c->min_dc = max_dc;
+    for (int32_t j = 0; j < m; ++j) c->min_dc = std::min(c->min_dc, cptr[j + 1] - cptr[j]);
     c->max_dv = max_dv;
     c->check_ptr.assign(cptr, cptr + m + 1);
     c->check_idx.assign(cidx, cidx + e);
