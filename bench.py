@@ -111,9 +111,11 @@ def main():
 
     H, g = load_code(torch.cuda.current_device())
     dev = torch.device("cuda", torch.cuda.current_device())
+    from qkd_ldpc_amd.dist import allreduce_counters, shard_range
     F = args.frames
     all_seeds = Q.make_seeds(args.seed, F * world)
-    seeds = torch.from_numpy(all_seeds[rank * F:(rank + 1) * F].view(np.int64)).to(dev)
+    b, e = shard_range(rank, world, F * world)          # weak scaling: F frames per rank
+    seeds = torch.from_numpy(all_seeds[b:e].view(np.int64)).to(dev)
     ws = Q.Workspace(H)
     stream = torch.cuda.current_stream()
 
@@ -124,7 +126,6 @@ def main():
     sp = torch.empty(F, dtype=torch.uint8, device=dev)
     ko = torch.empty(F, dtype=torch.uint8, device=dev)
     counters = torch.empty(Q._native.COUNTERS_BYTES, dtype=torch.uint8, device=dev)
-    cnt_u64 = counters.view(torch.int64)
     L = Q._native.lib()
     sptr = int(stream.cuda_stream)
 
@@ -139,7 +140,7 @@ def main():
         Q._native.check(L.qkd_counters_batch(iters.data_ptr(), sp.data_ptr(), ko.data_ptr(), F,
                                              counters.data_ptr(), H.device, sptr))
         if world > 1:
-            dist.all_reduce(cnt_u64[:5], op=dist.ReduceOp.SUM)
+            allreduce_counters(counters)
 
     for _ in range(args.warmup):
         step()

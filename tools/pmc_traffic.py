@@ -1,0 +1,39 @@
+"""HBM-side traffic of the decode kernel per launch from rocprofv3 --pmc passes
+(tools/gpu_pmc.sh: pass 1 FETCH_SIZE, pass 2 WRITE_SIZE), corrected as
+/opt/skills/guides/MI355X_MICROARCH.md prescribes for gfx950: FETCH_SIZE (KB)
+reports 1/2 of the bytes of wide reads -> x2; WRITE_SIZE (KB) as is.
+
+    python tools/pmc_traffic.py gpurun_out/pmc_1 gpurun_out/pmc_2 profiles/r01_pmc_decode.json
+"""
+import csv
+import json
+import os
+import sys
+
+
+def per_launch(d, counter):
+    vals = []
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        if "decode_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            vals.append(float(r["Counter_Value"]))
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    fetch_kb, nf = per_launch(sys.argv[1], "FETCH_SIZE")
+    write_kb, nw = per_launch(sys.argv[2], "WRITE_SIZE")
+    out = {
+        "kernel": "qkd::decode_kernel<1,6,true> (qkd_qkd_ldpc_batch, 4096 frames, QBER 0.02)",
+        "fetch_size_kb": fetch_kb,
+        "write_size_kb": write_kb,
+        "launches": [nf, nw],
+        "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B",
+        "hbm_bytes_per_launch": fetch_kb * 1024 * 2 + write_kb * 1024,
+    }
+    with open(sys.argv[3], "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
