@@ -123,31 +123,32 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) 
 }
 
 
+// Syndrome bit arrays hold whole 64-check groups (written by one ballot each).
+__host__ __device__ inline int decode_m_words(int m) { return ((m + 63) / 64) * 2; }
+
 // LDS layout of decode_kernel (bytes):
 //   total  [n_pad]          binary64 bit totals (the reference's `total`, :256-267)
-//   synm   [n_tasks]        target syndrome per wave task, one bit per lane
 //   tsyn   [m_words]        target syndrome, one bit per check
 //   xsyn   [m_words]        syndrome of the current hard decision (XOR-built)
 //   qsyn   [m_words]        QKD path: sign of each check's first-iteration product
 //   tval   [NW][64 + DC]    per-wave tanh values for the in-check products
-//                           (prologue: staged syndrome bytes / Alice+Bob words)
+//                           (prologue: the frame's Alice + Bob words)
 //   ctab   [kFirstTableDeg+1] first-iteration message magnitudes by degree
 //   tab2   [tab2_entries]   second-iteration tanh table
 //   t2idx  [n_pad]          per-bit base index into tab2 (uint16)
 //   ctl    [4]              frame index, block_any flags
 struct DecodeLds {
-    size_t synm, tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, bytes;
-    __host__ __device__ DecodeLds(int n_pad, int n_tasks, int m, int dc, int tab2_entries) {
-        const int m_words = (m + 31) / 32;
-        synm = (size_t)n_pad * 8;
-        tsyn = synm + (size_t)n_tasks * 8;
+    size_t tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, bytes;
+    __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries) {
+        const int m_words = decode_m_words(m);
+        tsyn = (size_t)n_pad * 8;
         xsyn = tsyn + (size_t)m_words * 4;
         qsyn = xsyn + (size_t)m_words * 4;
         tval = (qsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
-        // the tanh rows double as the prologue's staging area (syndrome bytes
-        // or Alice's words), so the region is at least that large
+        // the tanh rows double as the prologue's staging area for the frame's
+        // Alice and Bob words
         const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
-        const size_t stage = (size_t)m > (size_t)(n_pad / 64 + 1) * 16 ? (size_t)m : (size_t)(n_pad / 64 + 1) * 16;
+        const size_t stage = (size_t)n_words * 16;
         ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         t2idx = tab2 + (size_t)tab2_entries * 8;
@@ -191,7 +192,7 @@ enum CheckSrc : int {
 };
 
 template <int SRC, bool CLAMP, int DC>
-__device__ __forceinline__ double check_edge(double x, double old, uint32_t w, uint64_t sm, int lane,
+__device__ __forceinline__ double check_edge(double x, double old, uint32_t w, uint32_t sbit, int lane,
                                              double thr, double* row, int min_dc, uint32_t dummy) {
     if (SRC == kSrcGeneral) {
         x = x - old;
@@ -220,7 +221,7 @@ __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, u
     double o[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) o[k] = row[start + k];
-    double P = ((sm >> lane) & 1ull) ? -1.0 : 1.0;
+    double P = sbit ? -1.0 : 1.0;
     // factors below the code's smallest check degree belong to every lane
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
@@ -248,7 +249,7 @@ __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, u
 // The plan is padded with idle tasks (qkd_plan.h): no bounds tests on the
 // look-ahead loads.
 template <int SRC, bool CLAMP, int DC>
-__device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, const uint64_t* synm,
+__device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
                                             const double* total, const uint16_t* t2idx, const double* tab2,
                                             double* __restrict__ c2b, double* row,
                                             int n_tasks, int n_pad, double thr, int wave, int lane,
@@ -257,24 +258,26 @@ __device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, c
     constexpr bool FIRST = SRC != kSrcGeneral;    // no stored message is read
     int t = wave;
     if (t >= n_tasks) return;
-    const uint32_t* pl = plan + lane;
-    auto msg = [&](uint32_t w) -> double* { return c2b + pw_row(w) * n_pad + pw_bit(w); };
+    const uint2* pl = plan + lane;
+    auto msg = [&](uint2 p) -> double* { return c2b + pw_row(p.x) * n_pad + pw_bit(p.x); };
     // the incoming value: a bit total, or (kSrcTable) the tabulated tanh
-    auto src = [&](uint32_t w) -> double {
-        return SRC == kSrcTable ? tab2[t2idx[pw_bit(w)] + pw_row(w)] : total[pw_bit(w)];
+    auto src = [&](uint2 p) -> double {
+        return SRC == kSrcTable ? tab2[t2idx[pw_bit(p.x)] + pw_row(p.x)] : total[pw_bit(p.x)];
     };
-    uint32_t wa = pl[t * 64];
-    uint32_t wb = pl[(t + NW) * 64];
+    // the target syndrome bit of the lane's check
+    auto sbit = [&](uint2 p) -> uint32_t { return (tsyn[p.y >> 5] >> (p.y & 31)) & 1u; };
+    uint2 wa = pl[t * 64];
+    uint2 wb = pl[(t + NW) * 64];
     double xa = src(wa);
     double oa = FIRST ? 0.0 : *msg(wa);
     double* pend = nullptr;      // message computed by the previous task, not yet stored
     double pv = 0.0;
     for (;;) {
         if (pend) *pend = pv;
-        const uint32_t wc = pl[(t + 2 * NW) * 64];
+        const uint2 wc = pl[(t + 2 * NW) * 64];
         const double xb = src(wb);
         const double ob = FIRST ? 0.0 : *msg(wb);
-        pv = check_edge<SRC, CLAMP, DC>(xa, oa, wa, synm[t], lane, thr, row, min_dc, dummy);
+        pv = check_edge<SRC, CLAMP, DC>(xa, oa, wa.x, sbit(wa), lane, thr, row, min_dc, dummy);
         pend = msg(wa);
         t += NW;
         if (t >= n_tasks) break;
@@ -282,7 +285,7 @@ __device__ __forceinline__ void check_phase(const uint32_t* __restrict__ plan, c
         wa = pl[(t + 2 * NW) * 64];
         xa = src(wc);
         oa = FIRST ? 0.0 : *msg(wc);
-        pv = check_edge<SRC, CLAMP, DC>(xb, ob, wb, synm[t], lane, thr, row, min_dc, dummy);
+        pv = check_edge<SRC, CLAMP, DC>(xb, ob, wb.x, sbit(wb), lane, thr, row, min_dc, dummy);
         pend = msg(wb);
         t += NW;
         if (t >= n_tasks) break;
@@ -352,7 +355,7 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 // so every first-iteration message is +-C_d, bit for bit; the host evaluates
 // C_d with the same tanh/atanh restatement (decode_keys). sign_i is the sign
 // bit of the LLR in `total` (also right for log_p <= 0 and for +-0).
-__device__ __forceinline__ void first_check_phase(const uint32_t* __restrict__ plan, const uint64_t* synm,
+__device__ __forceinline__ void first_check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
                                                   const double* total, const double* ctab,
                                                   double* __restrict__ c2b, int n_tasks, int n_pad, int wave,
                                                   int lane) {
@@ -360,18 +363,18 @@ __device__ __forceinline__ void first_check_phase(const uint32_t* __restrict__ p
     // kPlanGroup tasks per trip: their plan words are loaded together (the
     // plan is padded, so the loads need no bounds test); stores are predicated.
     for (int t0 = wave; t0 < n_tasks; t0 += NW * kPlanGroup) {
-        uint32_t w[kPlanGroup];
+        uint2 w[kPlanGroup];
 #pragma unroll
         for (int u = 0; u < kPlanGroup; ++u) w[u] = plan[(t0 + u * NW) * 64 + lane];
 #pragma unroll
         for (int u = 0; u < kPlanGroup; ++u) {
             const int t = t0 + u * NW;
             if (t >= n_tasks) break;
-            const uint32_t bit = pw_bit(w[u]);
+            const uint32_t bit = pw_bit(w[u].x);
             const uint32_t sg = (uint32_t)qkdm::hi32(total[bit]) >> 31;
-            const uint32_t sp = (uint32_t)((synm[t] >> lane) & 1ull) ^ (uint32_t)seg_parity(__ballot(sg), w[u]);
-            const double cm = ctab[pw_deg(w[u])];
-            c2b[pw_row(w[u]) * n_pad + bit] = (sp ^ sg) ? -cm : cm;
+            const uint32_t sp = ((tsyn[w[u].y >> 5] >> (w[u].y & 31)) & 1u) ^ (uint32_t)seg_parity(__ballot(sg), w[u].x);
+            const double cm = ctab[pw_deg(w[u].x)];
+            c2b[pw_row(w[u].x) * n_pad + bit] = (sp ^ sg) ? -cm : cm;
         }
     }
 }
@@ -401,10 +404,9 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     constexpr int NW = kDecodeBlock / 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
-    const DecodeLds L(c.n_pad, c.n_tasks, c.m, DC, a.tab2_entries);
-    const int m_words = (c.m + 31) / 32;
+    const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries);
+    const int m_words = decode_m_words(c.m);
     double* total = reinterpret_cast<double*>(smem);
-    uint64_t* synm = reinterpret_cast<uint64_t*>(smem + L.synm);
     uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
     uint32_t* qsyn = reinterpret_cast<uint32_t*>(smem + L.qsyn);
@@ -422,7 +424,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     double* row = reinterpret_cast<double*>(smem + L.tval) + wave * (64 + DC);
     const int n_tasks = c.n_tasks;
     const int n_pad = c.n_pad;
-    const uint32_t* plan = c.plan;
+    const uint2* plan = c.plan;
     double* c2b = a.c2b + (size_t)blockIdx.x * a.c2b_stride;
     const double thr = a.thr;
     uint32_t any_k = 0;
@@ -437,15 +439,22 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     for (;;) {
         pc.mark(4);
         if (tid == 0) ctl[0] = atomicAdd(a.counter, 1u);
-        for (int w = tid; w < m_words; w += kDecodeBlock) {
-            tsyn[w] = 0;
-            xsyn[w] = 0;
-            qsyn[w] = 0;
-        }
+        for (int w = tid; w < m_words; w += kDecodeBlock) xsyn[w] = 0;
         __syncthreads();
         const uint32_t f = ctl[0];
         if (f >= a.n_frames) break;
 
+        // ---- prologue: the frame's Alice and Bob words staged in LDS (the tanh
+        //      rows are free until the first check phase)
+        const uint64_t* sw = reinterpret_cast<const uint64_t*>(smem + L.tval);   // [alice | bob]
+        if (MODE == kModeKeys) {
+            uint64_t* w = reinterpret_cast<uint64_t*>(smem + L.tval);
+            for (int q = tid; q < (int)a.words; q += kDecodeBlock) {
+                w[q] = a.alice_w[(size_t)f * a.words + q];
+                w[a.words + q] = a.bob_w[(size_t)f * a.words + q];
+            }
+            __syncthreads();
+        }
         // ---- prologue: channel LLRs into LDS (:188 / :400-405); the dummy
         //      column n of idle plan lanes gets 0
         uint32_t bobmask = 0;
@@ -456,8 +465,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                 if (MODE == kModeLlr) {
                     l = a.llr[(size_t)f * c.n + i];
                 } else {
-                    const uint64_t w = a.bob_w[(size_t)f * a.words + (i >> 6)];
-                    const uint32_t bb = (uint32_t)((w >> (i & 63)) & 1u);
+                    const uint32_t bb = (uint32_t)((sw[a.words + (i >> 6)] >> (i & 63)) & 1u);
                     bobmask |= bb << r;
                     l = bb ? -a.log_p : a.log_p;
                 }
@@ -465,59 +473,52 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             }
             if (tid == 0) total[c.n] = 0.0;
         }
-        // ---- prologue: target syndrome, per wave task and per check. The
-        //      frame's Alice words (or syndrome bytes) are staged in LDS (the
-        //      tanh rows are free until the first check phase), so each task
-        //      needs only its two coalesced plan loads.
-        {
-            uint8_t* stage = reinterpret_cast<uint8_t*>(smem + L.tval);
+        // ---- prologue: target syndrome bits per check (tsyn) and, on the QKD
+        //      path, each check's first-product sign (qsyn, fold_first_message);
+        //      thread per check, 64 consecutive checks per wave -> one ballot.
+        //      ELL pad entries are -1, so the row loads do not wait for the degree.
+        for (int j0 = wave * 64; j0 < c.m; j0 += kDecodeBlock) {
+            const int j = j0 + lane;
+            const bool ok = j < c.m;
+            int sj = 0, qj = 0;
             if (MODE == kModeLlr) {
-                for (int j = tid; j < c.m; j += kDecodeBlock) stage[j] = a.syn[(size_t)f * c.m + j] != 0;
+                sj = ok ? (a.syn[(size_t)f * c.m + j] != 0) : 0;
             } else {
-                uint64_t* sw = reinterpret_cast<uint64_t*>(stage);
-                for (int w = tid; w < (int)a.words; w += kDecodeBlock) {
-                    sw[w] = a.alice_w[(size_t)f * a.words + w];
-                    sw[a.words + w] = a.bob_w[(size_t)f * a.words + w];
+                // calculate_syndrome_irregular on Alice's key (:413-414), and
+                // q_j = s_j ^ syn(bob)_j ^ (deg_j & sign(log_p))
+                int bl[DC];
+#pragma unroll
+                for (int k = 0; k < DC; ++k) bl[k] = (ok && k < c.max_dc) ? c.chk_bits[k * c.m_pad + j] : -1;
+                uint32_t pa = 0, pb = 0, deg = 0;
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    const int bit = bl[k];
+                    if (bit >= 0) {
+                        pa ^= (uint32_t)(sw[bit >> 6] >> (bit & 63));
+                        pb ^= (uint32_t)(sw[a.words + (bit >> 6)] >> (bit & 63));
+                        deg++;
+                    }
                 }
+                if (ok && DC < c.max_dc) {
+                    for (int k = DC; k < c.max_dc; ++k) {
+                        const int bit = c.chk_bits[k * c.m_pad + j];
+                        if (bit >= 0) {
+                            pa ^= (uint32_t)(sw[bit >> 6] >> (bit & 63));
+                            pb ^= (uint32_t)(sw[a.words + (bit >> 6)] >> (bit & 63));
+                            deg++;
+                        }
+                    }
+                }
+                sj = (int)(pa & 1u);
+                qj = (int)((pa ^ pb ^ (lsign & deg)) & 1u);
             }
-            __syncthreads();
-            for (int t0 = wave; t0 < n_tasks; t0 += NW * kPlanGroup) {
-                uint32_t wg[kPlanGroup];
-                int jg[kPlanGroup];
-#pragma unroll
-                for (int u = 0; u < kPlanGroup; ++u) {
-                    wg[u] = plan[(t0 + u * NW) * 64 + lane];
-                    jg[u] = c.plan_chk[(t0 + u * NW) * 64 + lane];
-                }
-#pragma unroll
-                for (int u = 0; u < kPlanGroup; ++u) {
-                const int t = t0 + u * NW;
-                if (t >= n_tasks) break;
-                const uint32_t w = wg[u];
-                const int j = jg[u];
-                int s;
-                if (MODE == kModeLlr) {
-                    s = j >= 0 ? stage[j] : 0;
-                } else {
-                    // calculate_syndrome_irregular on Alice's key (:413-414)
-                    const uint32_t bit = pw_bit(w);
-                    const uint64_t* sw = reinterpret_cast<const uint64_t*>(stage);
-                    const int ab = j >= 0 ? (int)((sw[bit >> 6] >> (bit & 63)) & 1u) : 0;
-                    s = seg_parity(__ballot(ab), w);
-                }
-                const uint64_t sm = __ballot(s);
-                if (lane == 0) synm[t] = sm;
-                if (s && j >= 0 && lane == pw_start(w)) atomicOr(&tsyn[j >> 5], 1u << (j & 31));
-                if (MODE == kModeKeys && fold1) {
-                    // sign of the first-iteration product P of check j: s_j ^ the
-                    // sign bits of its LLRs (bob_i ^ sign(log_p)), fold_first_message
-                    const uint32_t bit = pw_bit(w);
-                    const uint64_t* bw = reinterpret_cast<const uint64_t*>(stage) + a.words;
-                    const int sg = j >= 0 ? (int)(((bw[bit >> 6] >> (bit & 63)) & 1u) ^ lsign) : 0;
-                    const int qs = s ^ seg_parity(__ballot(sg), w);
-                    if (qs && j >= 0 && lane == pw_start(w)) atomicOr(&qsyn[j >> 5], 1u << (j & 31));
-                }
-                }
+            const uint64_t sm = __ballot(sj);
+            const uint64_t qm = __ballot(qj);
+            if (lane == 0) {
+                tsyn[j0 >> 5] = (uint32_t)sm;
+                tsyn[(j0 >> 5) + 1] = (uint32_t)(sm >> 32);
+                qsyn[j0 >> 5] = (uint32_t)qm;
+                qsyn[(j0 >> 5) + 1] = (uint32_t)(qm >> 32);
             }
         }
         __syncthreads();
@@ -530,15 +531,15 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             if (it == 0 && fold1)
                 ;   // messages rebuilt from signs in the bit phase (fold_first_message)
             else if (it == 0 && MODE == kModeKeys && a.first_table)
-                first_check_phase(plan, synm, total, ctab, c2b, n_tasks, n_pad, wave, lane);
+                first_check_phase(plan, tsyn, total, ctab, c2b, n_tasks, n_pad, wave, lane);
             else if (it == 0)
-                check_phase<kSrcFirst, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
+                check_phase<kSrcFirst, CLAMP, DC>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
                                                   thr, wave, lane, c.min_dc, (uint32_t)c.n);
             else if (it == 1 && MODE == kModeKeys && a.tab2_entries)
-                check_phase<kSrcTable, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
+                check_phase<kSrcTable, CLAMP, DC>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
                                                   thr, wave, lane, c.min_dc, (uint32_t)c.n);
             else
-                check_phase<kSrcGeneral, CLAMP, DC>(plan, synm, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
+                check_phase<kSrcGeneral, CLAMP, DC>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
                                                     thr, wave, lane, c.min_dc, (uint32_t)c.n);
             __syncthreads();
             pc.mark((MODE == kModeKeys && it < 2 && a.first_table) ? 5 + (int)it : 1);
@@ -662,17 +663,30 @@ __global__ void syndrome_kernel(DeviceCode c, const uint8_t* bits, uint32_t n_fr
 }
 
 // ---- bit packing ------------------------------------------------------------
-// One lane per bit, one wave per 64-bit word: coalesced byte reads, one ballot.
+// One lane per 8 key bytes -> one packed byte (little-endian words, so the
+// byte array is the uint64 word array); bits past n are 0. 8-byte loads when
+// every frame row is 8-byte aligned (n % 8 == 0), byte loads otherwise.
 __global__ void pack_kernel(const uint8_t* bytes, uint32_t n, uint32_t words, uint32_t n_frames,
                             uint64_t* out) {
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t word = gid >> 6;                     // wave-uniform
-    if (word >= (size_t)n_frames * words) return;
-    const size_t f = word / words;
-    const uint32_t i = (uint32_t)(word - f * words) * 64 + (threadIdx.x & 63);
-    const int b = i < n ? (bytes[f * n + i] & 1) : 0;
-    const uint64_t v = __ballot(b);
-    if ((threadIdx.x & 63) == 0) out[word] = v;
+    const size_t per_frame = (size_t)words * 8;
+    if (gid >= (size_t)n_frames * per_frame) return;
+    const size_t f = gid / per_frame;
+    const uint32_t b = (uint32_t)(gid - f * per_frame);
+    const uint8_t* src = bytes + f * n;
+    uint32_t m = 0;
+    if ((n & 7u) == 0) {
+        if (b * 8 < n) {
+            const uint64_t v = *reinterpret_cast<const uint64_t*>(src + (size_t)b * 8) & 0x0101010101010101ull;
+            m = (uint32_t)((v * 0x0102040810204080ull) >> 56);   // byte k's LSB -> bit k
+        }
+    } else {
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t i = b * 8 + k;
+            if (i < n) m |= (uint32_t)(src[i] & 1u) << k;
+        }
+    }
+    reinterpret_cast<uint8_t*>(out)[gid] = (uint8_t)m;
 }
 
 __global__ void unpack_kernel(const uint64_t* words_in, uint32_t n, uint32_t words, uint32_t n_frames,
@@ -772,7 +786,7 @@ static DecodeFn pick_decode(int mode, bool clamp, int max_dc, int* dc) {
 }
 
 static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries) {
-    return DecodeLds(c->n_pad, c->n_tasks, c->m, dc, tab2_entries).bytes;
+    return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries).bytes;
 }
 
 // Resident workgroups of decode_kernel for this code on its device.
@@ -861,6 +875,8 @@ struct WsSession {
     }
 };
 
+static unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
 static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs& a, int mode,
                                 hipStream_t stream) {
     int dc = 0;
@@ -902,7 +918,6 @@ static qkd_status check_decode_params(uint32_t max_it, double thr, uint32_t flag
     return QKD_OK;
 }
 
-static unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace qkd
 
@@ -1027,9 +1042,9 @@ qkd_status qkd_qkd_ldpc_batch(const qkd_code* c, qkd_workspace* ws, const uint8_
     if (s != QKD_OK) return s;
     const uint32_t words = (uint32_t)((c->n + 63) / 64);
     const size_t nw = n_frames * words;
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 64, 256)), dim3(256), 0, (hipStream_t)stream, alice,
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 8, 256)), dim3(256), 0, (hipStream_t)stream, alice,
                        (uint32_t)c->n, words, (uint32_t)n_frames, ws->alice_w);
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 64, 256)), dim3(256), 0, (hipStream_t)stream, bob,
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 8, 256)), dim3(256), 0, (hipStream_t)stream, bob,
                        (uint32_t)c->n, words, (uint32_t)n_frames, ws->bob_w);
     QKD_HIP(hipGetLastError());
     return decode_keys(c, ws, n_frames, qber, max_iterations, msg_threshold, flags, bits_out, iterations,

@@ -47,9 +47,7 @@ static void free_device(qkd_code* c) {
     c->d_bit_pat = nullptr;
     c->d_pat_deg = nullptr;
     if (c->d_plan) (void)hipFree(c->d_plan);
-    if (c->d_plan_chk) (void)hipFree(c->d_plan_chk);
     c->d_plan = nullptr;
-    c->d_plan_chk = nullptr;
     c->d_chk_bits = nullptr;
     c->d_chk_deg = nullptr;
     c->d_bit_chk = nullptr;
@@ -201,12 +199,11 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
                           hipMemcpyHostToDevice));
         QKD_HIP(hipMemcpy(c->d_pat_deg, c->pat_deg.data(), c->pat_deg.size(), hipMemcpyHostToDevice));
     }
-    QKD_HIP(hipMalloc(&c->d_plan, plan.word.size() * sizeof(uint32_t)));
-    QKD_HIP(hipMalloc(&c->d_plan_chk, plan.chk.size() * sizeof(int32_t)));
-    QKD_HIP(hipMemcpy(c->d_plan, plan.word.data(), plan.word.size() * sizeof(uint32_t),
-                      hipMemcpyHostToDevice));
-    QKD_HIP(hipMemcpy(c->d_plan_chk, plan.chk.data(), plan.chk.size() * sizeof(int32_t),
-                      hipMemcpyHostToDevice));
+    std::vector<uint2> plan2(plan.word.size());
+    for (size_t k = 0; k < plan.word.size(); ++k)
+        plan2[k] = make_uint2(plan.word[k], plan.chk[k] < 0 ? 0u : (uint32_t)plan.chk[k]);
+    QKD_HIP(hipMalloc(&c->d_plan, plan2.size() * sizeof(uint2)));
+    QKD_HIP(hipMemcpy(c->d_plan, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
     return QKD_OK;
 }
 

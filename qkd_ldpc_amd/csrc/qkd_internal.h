@@ -29,8 +29,9 @@ constexpr int kMaxBitsLds = 20480;
 // Device-resident, immutable view of H.
 //   chk_bits[k * m_pad + j]  bit index of slot k of check j (ascending), -1 pad
 //                            (thread-per-check syndrome kernel)
-//   plan[s], plan_chk[s]     the check-phase wave plan (qkd_plan.h): slot
-//                            s = task*64 + lane holds one edge
+//   plan[s]                  the check-phase wave plan (qkd_plan.h): slot
+//                            s = task*64 + lane holds one edge: {plan word,
+//                            check index}
 //   bit_chk[k * n_pad + i]   k-th check of bit i (ascending), -1 pad
 //   bit_slot[k * n_pad + i]  plan slot of that edge (c2b messages are stored
 //                            per frame in plan order)
@@ -43,8 +44,7 @@ struct DeviceCode {
     int32_t n_tasks;
     const int32_t* chk_bits;
     const uint8_t* chk_deg;
-    const uint32_t* plan;
-    const int32_t* plan_chk;
+    const uint2* plan;            // {plan word, check index (0 on idle lanes)}
     const int32_t* bit_chk;
     const int32_t* bit_slot;
     const uint8_t* bit_deg;
@@ -89,8 +89,7 @@ struct qkd_code {
     int32_t* d_bit_chk = nullptr;
     int32_t* d_bit_slot = nullptr;
     uint8_t* d_bit_deg = nullptr;
-    uint32_t* d_plan = nullptr;
-    int32_t* d_plan_chk = nullptr;
+    uint2* d_plan = nullptr;
     int32_t n_pat = 0;                  // 0: too many degree patterns for the table
     std::vector<uint8_t> pat_deg;
     uint16_t* d_bit_pat = nullptr;
@@ -100,7 +99,7 @@ struct qkd_code {
 
     qkd::DeviceCode view() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, n_tasks,
-                               d_chk_bits, d_chk_deg, d_plan, d_plan_chk, d_bit_chk, d_bit_slot, d_bit_deg,
+                               d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_slot, d_bit_deg,
                                n_pat, d_bit_pat, d_pat_deg};
     }
 };
