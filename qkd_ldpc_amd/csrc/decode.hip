@@ -198,20 +198,7 @@ __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, u
         x = x - old;
         if (CLAMP) x = clamp_msg(x, thr);
     }
-    const double xh = x / 2.0;
-    // Saturated wave: every lane's |b2c/2| >= 22 (finite or inf, not NaN) or idle.
-    // Then tanh is exactly +-1 (tanh_flat's |x| >= 22 branch), the product is
-    // +-1, P/t = +-1 and 2*atanh(+-1) = +-inf, clamped to +-thr: the message is
-    // that value with the sign of P*t, bit for bit, without the transcendentals.
-    bool fast = false;
-    if (SRC == kSrcGeneral) {
-        const uint32_t ax = (uint32_t)qkdm::hi32(xh) & 0x7fffffffu;
-        const bool sat = (ax >= 0x40360000u && !(xh != xh)) || pw_bit(w) == dummy;
-        fast = __all(sat);
-    }
-    double tv;
-    if (fast) tv = __builtin_copysign(1.0, xh);
-    else tv = SRC == kSrcTable ? x : qkdm::tanh_flat(xh);
+    const double tv = SRC == kSrcTable ? x : qkdm::tanh_flat(x / 2.0);
     row[lane] = tv;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -222,17 +209,9 @@ __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, u
 #pragma unroll
     for (int k = 0; k < DC; ++k) o[k] = row[start + k];
     double P = sbit ? -1.0 : 1.0;
-    // factors below the code's smallest check degree belong to every lane
+    P = P * o[0];                         // every check has degree >= 1
 #pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        if (k < min_dc) P = P * o[k];
-        else P = k < deg ? P * o[k] : P;
-    }
-    if (fast) {
-        const double inf = __builtin_inf();
-        const double mag = CLAMP ? (inf > thr ? thr : inf) : inf;
-        return (P * tv) < 0.0 ? -mag : mag;      // P, tv are +-1: P/tv == P*tv
-    }
+    for (int k = 1; k < DC; ++k) P = k < deg ? P * o[k] : P;
     double v = 2.0 * qkdm::atanh_flat(P / tv);
     if (CLAMP) v = clamp_msg(v, thr);
     return v;
