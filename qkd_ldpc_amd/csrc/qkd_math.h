@@ -282,12 +282,13 @@ QKD_HD double atanh_ref(double x) {
 
 QKD_HD double sel(bool p, double a, double b) { return p ? a : b; }
 
-// expm1 restricted to the arguments tanh feeds it:
-//   a in [-2, -2^-54]  (tanh of 2^-55 <= |x| < 1: expm1(-2|x|))
-//   a in [ 2,  44)     (tanh of 1 <= |x| < 22:    expm1( 2|x|))
+// expm1 restricted to the arguments tanh_flat feeds it:
+//   a in (-2, 0]  (tanh of |x| < 1: expm1(-2|x|), tiny and zero included)
+//   a in [2, 64]  (tanh of |x| >= 1: expm1(min(2|x|, 64)))
 // On this domain the reference's expm1 takes only these paths:
-//   k = 0 (|a| <= ln2/2), k = -1 (ln2/2 < |a| < 1.5 ln2, a < 0), general
-//   k in {-3,-2} or [3, 64]; no overflow, no k = 1, no k = 1024.
+//   k = 0 (|a| <= ln2/2; below 2^-54 it returns a, which the k = 0 formula
+//   reproduces: a + a^2/2 rounds to a), k = -1 (ln2/2 < |a| < 1.5 ln2, a < 0),
+//   general k in {-3,-2} or [3, 93]; no overflow, no k = 1, no k = 1024.
 QKD_HD double expm1_tanh_domain(double x) {
     const double ln2_hi = 6.93147180369123816490e-01;
     const double ln2_lo = 1.90821492927058770002e-10;
@@ -341,20 +342,22 @@ QKD_HD double expm1_tanh_domain(double x) {
 }
 
 QKD_HD double tanh_flat(double x) {
-    const int32_t jx = hi32(x);
-    const int32_t ix = jx & 0x7fffffff;
-    const double ax = __builtin_fabs(x);
-    const bool ge1 = ix >= 0x3ff00000;
-    const bool body = ix >= 0x3c800000 && ix < 0x40360000;     // 2^-55 <= |x| < 22
-    const double a = body ? (ge1 ? 2.0 * ax : -2.0 * ax) : 2.0;
+    const uint32_t ix = (uint32_t)hi32(x) & 0x7fffffffu;
+    const bool ge1 = ix >= 0x3ff00000u;
+    // One expm1 argument for every input:
+    //   |x| <  2^-55 (and +-0, subnormals): a = -2|x|; expm1's k = 0 branch then
+    //     returns a exactly, q = |x| exactly, so the result is x, as the
+    //     reference's x*(1+x) (1+x rounds to 1).
+    //   |x| >= 22, +-inf, NaN: a = min(2|x|, 64) >= 44, so 2/(t+2) < 2^-54 and
+    //     1 - q rounds to exactly 1.0, the reference's |x| >= 22 value (NaN is
+    //     replaced below).
+    const double aa = __builtin_fmin(2.0 * __builtin_fabs(x), 64.0);
+    const double a = ge1 ? aa : -aa;
     const double t = expm1_tanh_domain(a);
     const double q = (ge1 ? 2.0 : -t) / (t + 2.0);            // 2/(t+2) or -t/(t+2)
-    double z = ge1 ? 1.0 - q : q;
-    z = ix >= 0x40360000 ? 1.0 : z;                           // |x| >= 22
-    double r = jx >= 0 ? z : -z;
-    r = ix < 0x3c800000 ? x * (1.0 + x) : r;                  // tiny and +-0 (x*(1+x) == x)
-    const double sp = x != x ? x + x : (jx >= 0 ? 1.0 : -1.0); // NaN / +-inf
-    return ix >= 0x7ff00000 ? sp : r;
+    const double z = ge1 ? 1.0 - q : q;
+    const double r = __builtin_copysign(z, x);
+    return x != x ? x : r;
 }
 
 // log1p restricted to the arguments atanh feeds it: x in [2^-27, 2^54],
@@ -386,19 +389,22 @@ QKD_HD double log1p_atanh_domain(double x) {
     k = lowm ? k : k + 1;
     hu = lowm ? hu : (0x00100000 - hu) >> 2;
     double f = u - 1.0;
-    // k = 0 path
+    // k = 0 path (on the other path k >= 1: u = 1 + x >= sqrt 2 is halved)
     f = k0 ? x : f;
     k = k0 ? 0 : k;
     hu = k0 ? 1 : hu;
     c = k0 ? 0.0 : c;
 
+    // The reference's k = 0 formulas equal its general ones at k = 0, c = 0:
+    //   0*ln2_hi - ((A - (0*ln2_lo + 0)) - f) = -(A - f) = f - A  (rounding is
+    //   symmetric under negation; the zero cases give +0 both ways), so one
+    //   formula serves both.
     const double hfsq = 0.5 * f * f;
     const double dk = (double)k;
+    const double cl = dk * ln2_lo + c;
     // |f| < 2^-20 tails (hu == 0)
     const double R0 = hfsq * (1.0 - 0.66666666666666666 * f);
-    const double tail_f0 = k == 0 ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
-    const double tail_r = k == 0 ? f - R0 : dk * ln2_hi - ((R0 - (dk * ln2_lo + c)) - f);
-    const double tail = f == 0.0 ? tail_f0 : tail_r;
+    const double tail = f == 0.0 ? dk * ln2_hi + cl : dk * ln2_hi - ((R0 - cl) - f);
     // main
     const double s = f / (2.0 + f);
     const double z = s * s;
@@ -410,8 +416,7 @@ QKD_HD double log1p_atanh_domain(double x) {
     const double z6 = z4 * z2;
     const double R4 = Lp6 + z * Lp7;
     const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
-    const double m = k == 0 ? f - (hfsq - s * (hfsq + R))
-                            : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+    const double m = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + cl)) - f);
     return hu == 0 ? tail : m;
 }
 
@@ -421,13 +426,13 @@ QKD_HD double atanh_flat(double x) {
     const double t = xa + xa;
     const double q = (small ? t * xa : t) / (1.0 - xa);      // t*xa/(1-xa) or (xa+xa)/(1-xa)
     const double arg = small ? t + q : q;
-    const bool body = xa >= 0x1.0p-28 && xa < 1.0;            // false for NaN
-    const double r = 0.5 * log1p_atanh_domain(body ? arg : 1.0);
+    // |x| >= 1 and NaN pass meaningless arguments through log1p (integer work
+    // on bit patterns only: no traps, no undefined behaviour); replaced below
+    const double r = 0.5 * log1p_atanh_domain(arg);
     const double res = __builtin_copysign(r, x);
-    // |x| >= 1 or NaN: +-1 -> +-inf, |x| > 1 -> NaN, NaN -> NaN
-    const double inf = __builtin_copysign(__builtin_inf(), x);
-    const double sp = xa == 1.0 ? inf : (x != x ? x + x : __builtin_nan(""));
-    return xa < 0x1.0p-28 ? x : (body ? res : sp);
+    // +-1 -> +-inf; |x| > 1 and NaN -> NaN (payloads never reach an output)
+    const double sp = xa == 1.0 ? __builtin_copysign(__builtin_inf(), x) : __builtin_nan("");
+    return xa < 0x1.0p-28 ? x : (xa < 1.0 ? res : sp);
 }
 
 }  // namespace qkdm
