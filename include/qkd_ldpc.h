@@ -182,6 +182,10 @@ QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t 
  * reference counterpart (the reference prints TRACE_* arrays instead,
  * qkd_ldpc_algorithm.cpp:42-155). */
 QKD_API qkd_status qkd_debug_phase_cycles(qkd_workspace *ws, uint64_t *cycles7);
+/* The decoder's tanh (which = 0) / atanh (which = 1) restatement applied to
+ * x[n] -> y[n] (device arrays): the bit-exactness check of the device build
+ * against glibc (reference qkd_ldpc_algorithm.cpp:224, :241). */
+QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
 
 /* ---- host helpers --------------------------------------------------------- */
 /* seeds[k] = k-th raw xoshiro256++(simulation_seed) output (simulation.cpp:222-228). */

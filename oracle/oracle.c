@@ -504,3 +504,9 @@ ORC_API int orc_trials(const orc_code *h, double q_nom, const uint64_t *seeds, u
     pthread_mutex_destroy(&j.mu);
     return j.err ? -1 : 0;
 }
+
+/* glibc tanh / atanh over arrays (the reference calls them per message,
+ * qkd_ldpc_algorithm.cpp:224,241): the checker of the device restatement. */
+ORC_API void orc_libm_array(int which, const double *x, double *y, size_t n) {
+    for (size_t i = 0; i < n; i++) y[i] = which == 0 ? tanh(x[i]) : atanh(x[i]);
+}

@@ -45,6 +45,7 @@ def lib():
         L.orc_code_dims.argtypes = [P, i32p]
         L.orc_code_lists.argtypes = [P, i32p, i32p, i32p, i32p]
         L.orc_seeds.argtypes = [C.c_uint64, C.c_size_t, u64p]
+        L.orc_libm_array.argtypes = [C.c_int, f64p, f64p, C.c_size_t]
         L.orc_keygen.restype = C.c_double
         L.orc_keygen.argtypes = [C.c_uint64, C.c_int, C.c_double, i32p, i32p]
         L.orc_syndrome.argtypes = [P, i32p, i32p]
@@ -169,6 +170,14 @@ class Code:
         if rc != 0:
             raise RuntimeError(f"Key size '{self.n}' is too small for QBER.")
         return {"iters": it, "sp_ok": sp.astype(bool), "key_ok": ko.astype(bool), "exact_q": q}
+
+
+def libm(which: str, x) -> np.ndarray:
+    """glibc tanh ('tanh') or atanh ('atanh') of every element."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_libm_array(0 if which == "tanh" else 1, x, y, x.size)
+    return y
 
 
 def seeds(sim_seed: int, count: int) -> np.ndarray:

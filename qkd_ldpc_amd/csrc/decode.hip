@@ -1070,6 +1070,21 @@ qkd_status qkd_keygen_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t
     return QKD_OK;
 }
 
+__global__ void math_kernel(int which, const double* x, double* y, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = which == 0 ? qkdm::tanh_flat(x[i]) : qkdm::atanh_flat(x[i]);
+}
+
+qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void* stream) {
+    clear_error();
+    if (!x || !y || (which != 0 && which != 1)) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if (n == 0) return QKD_OK;
+    hipLaunchKernelGGL(math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, which,
+                       x, y, n);
+    QKD_HIP(hipGetLastError());
+    return QKD_OK;
+}
+
 qkd_status qkd_debug_phase_cycles(qkd_workspace* ws, uint64_t* cycles7) {
     if (!ws || !cycles7) return set_error(QKD_ERR_INVALID_ARG, "null argument");
     if (!ws->counter) return set_error(QKD_ERR_INVALID_ARG, "workspace has not decoded yet");

@@ -280,7 +280,28 @@ QKD_HD double atanh_ref(double x) {
 // checks them against glibc and against the path-by-path forms).
 // ===========================================================================
 
-QKD_HD double sel(bool p, double a, double b) { return p ? a : b; }
+// a / b for operands the callers keep in the normal range: |a|, |b| and |a/b|
+// in [2^-107, 2^64] (or a = +0 with b > 0). On gfx950 the compiler's IEEE
+// division is v_div_scale x2, v_rcp, the Newton/Markstein fma chain,
+// v_div_fmas and v_div_fixup; for such operands div_scale returns its input
+// unchanged with VCC = 0, div_fmas is then a plain fma and div_fixup returns
+// its first operand, so the chain below is the same sequence of roundings and
+// the correctly rounded quotient, three instructions shorter. The host build
+// divides.
+QKD_HD double div_normal(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double r0 = __builtin_amdgcn_rcp(b);
+    const double e0 = __builtin_fma(-b, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-b, r1, 1.0);
+    const double r2 = __builtin_fma(r1, e1, r1);
+    const double q0 = a * r2;
+    const double rem = __builtin_fma(-b, q0, a);
+    return __builtin_fma(rem, r2, q0);
+#else
+    return a / b;
+#endif
+}
 
 // expm1 restricted to the arguments tanh_flat feeds it:
 //   a in (-2, 0]  (tanh of |x| < 1: expm1(-2|x|), tiny and zero included)
@@ -323,7 +344,7 @@ QKD_HD double expm1_tanh_domain(double x) {
     const double R3 = Q4 + hxs * Q5;
     const double r1 = R1 + h2 * R2 + h4 * R3;
     const double t = 3.0 - r1 * hfx;
-    const double e = hxs * ((r1 - t) / (6.0 - xr * t));
+    const double e = hxs * div_normal(r1 - t, 6.0 - xr * t);   // ~ -2 / [5, 7]
 
     const double res0 = xr - (xr * e - hxs);                 // k == 0
     const double e2 = (xr * (e - c) - c) - hxs;              // k != 0
@@ -354,7 +375,9 @@ QKD_HD double tanh_flat(double x) {
     const double aa = __builtin_fmin(2.0 * __builtin_fabs(x), 64.0);
     const double a = ge1 ? aa : -aa;
     const double t = expm1_tanh_domain(a);
-    const double q = (ge1 ? 2.0 : -t) / (t + 2.0);            // 2/(t+2) or -t/(t+2)
+    // 2/(t+2) or -t/(t+2); t+2 in [1.13, 2^93], numerator 2 or in [2^-55, 0.87]
+    // (+0 for x = +-0; subnormal-range x divides a subnormal by exactly 2)
+    const double q = div_normal(ge1 ? 2.0 : -t, t + 2.0);
     const double z = ge1 ? 1.0 - q : q;
     const double r = __builtin_copysign(z, x);
     return x != x ? x : r;
@@ -382,7 +405,8 @@ QKD_HD double log1p_atanh_domain(double x) {
     int32_t hu = hi32(u);
     int32_t k = (hu >> 20) - 1023;
     double c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0);
-    c = huge ? 0.0 : c / u;
+    // c: the rounding error of 1 + x, 0 or a multiple of ulp(x) >= 2^-54; u in [1.41, 2^53]
+    c = huge ? 0.0 : div_normal(c, u);
     hu &= 0x000fffff;
     const bool lowm = hu < 0x6a09e;
     u = set_hi32(u, (uint32_t)hu | (lowm ? 0x3ff00000u : 0x3fe00000u));
@@ -406,7 +430,7 @@ QKD_HD double log1p_atanh_domain(double x) {
     const double R0 = hfsq * (1.0 - 0.66666666666666666 * f);
     const double tail = f == 0.0 ? dk * ln2_hi + cl : dk * ln2_hi - ((R0 - cl) - f);
     // main
-    const double s = f / (2.0 + f);
+    const double s = div_normal(f, 2.0 + f);                  // f in [2^-54, 0.42], or 0
     const double z = s * s;
     const double R1 = z * Lp1;
     const double z2 = z * z;
@@ -424,7 +448,9 @@ QKD_HD double atanh_flat(double x) {
     const double xa = __builtin_fabs(x);
     const bool small = xa < 0.5;
     const double t = xa + xa;
-    const double q = (small ? t * xa : t) / (1.0 - xa);      // t*xa/(1-xa) or (xa+xa)/(1-xa)
+    // t*xa/(1-xa) or (xa+xa)/(1-xa): for 2^-28 <= xa < 1 numerator in [2^-55, 2),
+    // 1 - xa in [2^-53, 1]; other lanes are replaced below
+    const double q = div_normal(small ? t * xa : t, 1.0 - xa);
     const double arg = small ? t + q : q;
     // |x| >= 1 and NaN pass meaningless arguments through log1p (integer work
     // on bit patterns only: no traps, no undefined behaviour); replaced below

@@ -293,3 +293,38 @@ def test_qkd_ldpc_iteration_caps_inside_tables(Q, H, oracle_code, max_it):
     alice = rng.integers(0, 2, (4, 10240))
     bob = alice ^ (rng.random((4, 10240)) < 0.05)
     _qkd_both(Q, H, oracle_code, alice, bob, 0.05, max_it, 100.0, True)
+
+
+# ---- the device transcendentals against glibc ---------------------------------------------
+
+def _math_inputs(seed):
+    rng = np.random.default_rng(seed)
+    u = rng.uniform(-1.0, 1.0, 400_000)
+    parts = [u * 60.0, np.ldexp(u, rng.integers(-66, 6, u.size)),
+             np.ldexp(np.round(u * 64.0), -5), u, np.ldexp(u, -rng.integers(0, 60, u.size)),
+             np.copysign(1.0 - np.ldexp(np.abs(u), -rng.integers(0, 54, u.size)), u),
+             np.nextafter(np.copysign(1.0, u), 0.0),
+             rng.integers(0, 2**63, u.size, dtype=np.int64).view(np.float64)]
+    ex = np.arange(-1075, 1025)
+    mant = 1.0 + np.arange(64) / 64.0
+    sweep = np.ldexp(mant[None, :], ex[:, None]).ravel()
+    sp = np.array([0.0, -0.0, 1.0, -1.0, 22.0, -22.0, 0.5, -0.5, np.inf, -np.inf, np.nan,
+                   2.0**-28, 2.0**-55, 2.0**-54, 709.78, -38.0, 0.41422, 5e-324, -5e-324])
+    return np.concatenate(parts + [sweep, -sweep, np.nextafter(sweep, 0.0), sp])
+
+
+@pytest.mark.parametrize("which", ["tanh", "atanh"])
+def test_device_math_bit_exact_vs_glibc(Q, oracle_mod, which):
+    """The device build of qkd_math.h's flat tanh/atanh (with its shortened
+    divisions) equals glibc 2.35 bit for bit (NaN payloads aside)."""
+    x = _math_inputs(17 if which == "tanh" else 23)
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.empty_like(dx)
+    Q._native.check(Q._native.lib().qkd_debug_math(0 if which == "tanh" else 1, dx.data_ptr(),
+                                                   dy.data_ptr(), x.size, None))
+    torch.cuda.synchronize()
+    got = dy.cpu().numpy()
+    want = oracle_mod.libm(which, x)
+    same = (got.view(np.uint64) == want.view(np.uint64)) | (np.isnan(got) & np.isnan(want))
+    bad = np.nonzero(~same)[0]
+    assert bad.size == 0, [(float.hex(x[i]), float.hex(got[i]), float.hex(want[i])) for i in bad[:5]]
