@@ -48,6 +48,8 @@ static void free_device(qkd_code* c) {
     c->d_pat_deg = nullptr;
     if (c->d_plan) (void)hipFree(c->d_plan);
     c->d_plan = nullptr;
+    if (c->d_jump) (void)hipFree(c->d_jump);
+    c->d_jump = nullptr;
     c->d_chk_bits = nullptr;
     c->d_chk_deg = nullptr;
     c->d_bit_chk = nullptr;
@@ -204,6 +206,15 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         plan2[k] = make_uint2(plan.word[k], plan.chk[k] < 0 ? 0u : (uint32_t)plan.chk[k]);
     QKD_HIP(hipMalloc(&c->d_plan, plan2.size() * sizeof(uint2)));
     QKD_HIP(hipMemcpy(c->d_plan, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    // Key-generation jump-ahead: chunk = draws per lane, a multiple of 64 so
+    // every lane's Alice bits fill whole words.
+    const uint64_t draws = qkdr::trial_draws((uint32_t)n);
+    const uint64_t per_lane = (draws + kKeygenLanes - 1) / kKeygenLanes;
+    c->keygen_chunk = (uint32_t)((per_lane + 63) / 64 * 64);
+    std::vector<uint64_t> jump((size_t)kKeygenLevels * 256 * 4);
+    qkdr::xoshiro_jump_matrices(c->keygen_chunk, kKeygenLevels, jump.data());
+    QKD_HIP(hipMalloc(&c->d_jump, jump.size() * sizeof(uint64_t)));
+    QKD_HIP(hipMemcpy(c->d_jump, jump.data(), jump.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
     return QKD_OK;
 }
 

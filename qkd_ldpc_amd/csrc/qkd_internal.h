@@ -25,6 +25,11 @@ __host__ __device__ inline int tab2_stride(int max_dv) { return (1 << (1 + max_d
 constexpr int kMaxCheckDegree = 64;
 // The per-frame bit totals live in LDS as binary64: N <= this.
 constexpr int kMaxBitsLds = 20480;
+// Parallel key generation: 64 lanes per frame, jump levels log2(64); frames
+// with more flipped positions than this take the serial kernel.
+constexpr int kKeygenLanes = 64;
+constexpr int kKeygenLevels = 6;
+constexpr uint32_t kKeygenFastMaxErrors = 4096;
 
 // Device-resident, immutable view of H.
 //   chk_bits[k * m_pad + j]  bit index of slot k of check j (ascending), -1 pad
@@ -94,6 +99,10 @@ struct qkd_code {
     std::vector<uint8_t> pat_deg;
     uint16_t* d_bit_pat = nullptr;
     uint8_t* d_pat_deg = nullptr;
+    // parallel key generation (decode.hip: keygen_fast_kernel): lane l of a
+    // frame's wave starts at draw l * keygen_chunk; d_jump[b] = T^(chunk * 2^b)
+    uint32_t keygen_chunk = 0;
+    uint64_t* d_jump = nullptr;
     int cu_count = 0;
     qkd_workspace* default_ws = nullptr;
 

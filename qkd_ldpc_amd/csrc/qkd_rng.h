@@ -126,4 +126,98 @@ QKD_RHD void shuffle_low_positions(Xoshiro256pp& g, uint32_t n, uint32_t ne, Low
     }
 }
 
+// ---------------------------------------------------------------------------
+// Jump-ahead for the parallel key generator (decode.hip: keygen_fast_kernel).
+//
+// xoshiro256's state transition (next() without its output scrambler) is
+// linear over GF(2)^256, so "advance by j draws" is a 256x256 bit matrix T^j.
+// A matrix is stored as 256 columns of 4 words: column k is the image of the
+// unit state with bit k set (bits 0..63 = s0, ..., 192..255 = s3).
+// ---------------------------------------------------------------------------
+
+QKD_RHD void xoshiro_step_state(uint64_t s[4]) {
+    const uint64_t t = s[1] << 17;
+    s[2] ^= s[0];
+    s[3] ^= s[1];
+    s[1] ^= s[2];
+    s[0] ^= s[3];
+    s[2] ^= t;
+    s[3] = (s[3] << 45) | (s[3] >> 19);
+}
+
+// s <- M s
+QKD_RHD void jump_apply(const uint64_t* cols, uint64_t s[4]) {
+    uint64_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+    for (int w = 0; w < 4; ++w) {
+        const uint64_t sw = s[w];
+        const uint64_t* c = cols + (size_t)w * 64 * 4;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 8
+#endif
+        for (int j = 0; j < 64; ++j) {
+            const uint64_t m = (uint64_t)0 - ((sw >> j) & 1u);
+            o0 ^= c[j * 4 + 0] & m;
+            o1 ^= c[j * 4 + 1] & m;
+            o2 ^= c[j * 4 + 2] & m;
+            o3 ^= c[j * 4 + 3] & m;
+        }
+    }
+    s[0] = o0;
+    s[1] = o1;
+    s[2] = o2;
+    s[3] = o3;
+}
+
+// Host: out[b] = T^(chunk * 2^b), b = 0..levels-1 (levels * 256 * 4 words).
+inline void xoshiro_jump_matrices(uint64_t chunk, int levels, uint64_t* out) {
+    const size_t MW = 256 * 4;
+    uint64_t* T = new uint64_t[MW];
+    uint64_t* R = new uint64_t[MW];
+    uint64_t* tmp = new uint64_t[MW];
+    for (int k = 0; k < 256; ++k) {
+        uint64_t v[4] = {0, 0, 0, 0};
+        v[k >> 6] = 1ull << (k & 63);
+        xoshiro_step_state(v);
+        for (int w = 0; w < 4; ++w) T[k * 4 + w] = v[w];
+    }
+    // mul(A, B) = A * B, column by column: (A B) e_k = A (B e_k)
+    auto mul = [&](const uint64_t* A, const uint64_t* B, uint64_t* C) {
+        for (int k = 0; k < 256; ++k) {
+            uint64_t v[4] = {B[k * 4], B[k * 4 + 1], B[k * 4 + 2], B[k * 4 + 3]};
+            jump_apply(A, v);
+            for (int w = 0; w < 4; ++w) C[k * 4 + w] = v[w];
+        }
+    };
+    // R = T^chunk (square and multiply)
+    for (int k = 0; k < 256; ++k) {
+        for (int w = 0; w < 4; ++w) R[k * 4 + w] = 0;
+        R[k * 4 + (k >> 6)] = 1ull << (k & 63);
+    }
+    uint64_t e = chunk;
+    while (e) {
+        if (e & 1) {
+            mul(T, R, tmp);
+            for (size_t i = 0; i < MW; ++i) R[i] = tmp[i];
+        }
+        mul(T, T, tmp);
+        for (size_t i = 0; i < MW; ++i) T[i] = tmp[i];
+        e >>= 1;
+    }
+    for (int b = 0; b < levels; ++b) {
+        for (size_t i = 0; i < MW; ++i) out[b * MW + i] = R[i];
+        mul(R, R, tmp);
+        for (size_t i = 0; i < MW; ++i) R[i] = tmp[i];
+    }
+    delete[] T;
+    delete[] R;
+    delete[] tmp;
+}
+
+// Draw count of one trial: N alice bits, the lone swap draw (even N), one
+// Lemire draw per shuffle pair (std::shuffle, see shuffle_low_positions),
+// without rejections.
+QKD_RHD uint64_t trial_draws(uint32_t n) {
+    return (n & 1u) == 0 ? (uint64_t)n + 1 + (n >= 2 ? (n - 2) / 2 : 0) : (uint64_t)n + (n - 1) / 2;
+}
+
 }  // namespace qkdr

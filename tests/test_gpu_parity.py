@@ -328,3 +328,27 @@ def test_device_math_bit_exact_vs_glibc(Q, oracle_mod, which):
     same = (got.view(np.uint64) == want.view(np.uint64)) | (np.isnan(got) & np.isnan(want))
     bad = np.nonzero(~same)[0]
     assert bad.size == 0, [(float.hex(x[i]), float.hex(got[i]), float.hex(want[i])) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("mode", ["fast", "replay", "serial"])
+def test_keygen_kernels_agree_with_oracle(Q, oracle_mod, monkeypatch, mode):
+    """The wave-per-frame jump-ahead generator (default), its in-wave serial
+    regeneration (taken after a Lemire rejection; forced here) and the
+    one-thread-per-frame kernel all reproduce run_trial's keys."""
+    if mode != "fast":
+        monkeypatch.setenv("QKD_KEYGEN", mode)
+    rng = np.random.default_rng(31)
+    for n, q in [(2, 0.5), (3, 1.0), (6, 0.5), (10, 1.0), (64, 0.1), (65, 0.5), (127, 0.3),
+                 (1001, 0.02), (4100, 1.0), (10240, 0.3), (10240, 0.45)]:
+        dense = np.zeros((n - 1, n), np.uint8)
+        for j in range(n - 1):
+            dense[j, j] = dense[j, j + 1] = 1
+        H = Q.HMatrix.from_dense_array(dense)
+        seeds = rng.integers(0, 2**63, 6, dtype=np.int64).astype(np.uint64)
+        a, b, qq = Q.keygen(H, seeds_dev(seeds), q)
+        torch.cuda.synchronize()
+        a, b, qq = a.cpu().numpy(), b.cpu().numpy(), qq.cpu().numpy()
+        for f, s in enumerate(seeds):
+            wa, wb, wq = oracle_mod.keygen(int(s), n, q)
+            assert (a[f] == wa).all() and (b[f] == wb).all(), (mode, n, q, f)
+            assert qq[f] == wq

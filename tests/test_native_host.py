@@ -27,6 +27,17 @@ def rng_bin(tmp_path_factory):
     return _build(tmp_path_factory, "rng_check")
 
 
+@pytest.fixture(scope="module")
+def jump_bin(tmp_path_factory):
+    return _build(tmp_path_factory, "jump_check")
+
+
+def test_xoshiro_jump_matrices_equal_stepping(jump_bin):
+    """The key generator's jump-ahead (lane l starts at draw l * chunk) equals
+    stepping the generator l * chunk times, for several chunks and seeds."""
+    assert subprocess.check_output([jump_bin], text=True).strip() == "0"
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_math_bit_exact_vs_glibc(math_bin, seed):
     out = subprocess.check_output([math_bin, "400000", str(seed)], text=True)
