@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -153,7 +154,23 @@ ThreadCtx& ctx() {
     return *c;
 }
 
-uint32_t flags_from_cfg() { return CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD ? QKD_FLAG_THRESHOLD : 0u; }
+// The reference's only decoder switch is the clamp. QKD_AMD_VARIANT=sp_f32 |
+// minsum selects one of the library's binary32 variants for a whole run (the
+// default, sp_f64, is the reference's decoder bit for bit).
+uint32_t variant_from_env() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("QKD_AMD_VARIANT");
+        if (!e || !*e || !std::strcmp(e, "sp_f64")) return QKD_VARIANT_SP_F64;
+        if (!std::strcmp(e, "sp_f32")) return QKD_VARIANT_SP_F32;
+        if (!std::strcmp(e, "minsum")) return QKD_VARIANT_MINSUM;
+        throw std::runtime_error(std::string("QKD_AMD_VARIANT: unknown decoder variant '") + e + "'");
+    }();
+    return v;
+}
+
+uint32_t flags_from_cfg() {
+    return (CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD ? QKD_FLAG_THRESHOLD : 0u) | variant_from_env();
+}
 
 // The reference's `while (curr_iteration != max_num_iterations)` runs zero
 // iterations for 0; the ABI takes >= 1, so 0 is answered here.

@@ -62,6 +62,24 @@ typedef enum qkd_status {
 #define QKD_FLAG_THRESHOLD 0x1u  /* CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD
                                     (qkd_ldpc_algorithm.cpp:246,313)         */
 
+/* Check-node rule (flag bits 4-5). QKD_VARIANT_SP_F64 is the reference's
+ * decoder (qkd_ldpc_algorithm.cpp:175-345), bit-exact. The other two are
+ * build-defined variants with binary32 messages and totals (SURVEY.md §8(d),
+ * config 5): same flooding schedule, stopping rule, clamp and outputs; their
+ * frame error rates are compared with the reference's, not their frames. */
+#define QKD_VARIANT_MASK   0x30u
+#define QKD_VARIANT_SP_F64 0x00u  /* sum-product, binary64 (the reference)    */
+#define QKD_VARIANT_SP_F32 0x10u  /* sum-product, binary32, OCML tanhf/atanhf;
+                                     |P/t| limited to 1 - 2^-24             */
+#define QKD_VARIANT_MINSUM 0x20u  /* normalised min-sum, binary32:
+                                     c2b = scale * sign * min |b2c| over the
+                                     check's other edges                     */
+/* Min-sum scale in flag bits 8-15 as round(scale * 256); 0 selects
+ * QKD_MINSUM_DEFAULT_SCALE. */
+#define QKD_MINSUM_SCALE_SHIFT 8
+#define QKD_MINSUM_SCALE(x) ((((uint32_t)((x) * 256.0 + 0.5)) & 0xffu) << QKD_MINSUM_SCALE_SHIFT)
+#define QKD_MINSUM_DEFAULT_SCALE 0.8125  /* best FER of {0.625..0.875} on config 3 */
+
 typedef struct qkd_code qkd_code;
 typedef struct qkd_workspace qkd_workspace;
 
@@ -184,7 +202,9 @@ QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t 
 QKD_API qkd_status qkd_debug_phase_cycles(qkd_workspace *ws, uint64_t *cycles7);
 /* The decoder's tanh (which = 0) / atanh (which = 1) restatement applied to
  * x[n] -> y[n] (device arrays): the bit-exactness check of the device build
- * against glibc (reference qkd_ldpc_algorithm.cpp:224, :241). */
+ * against glibc (reference qkd_ldpc_algorithm.cpp:224, :241). which = 2 / 3:
+ * the binary32 variant's tanh(x/2) / 2*atanh(x) (QKD_VARIANT_SP_F32), x
+ * rounded to binary32, result widened. */
 QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
 
 /* ---- host helpers --------------------------------------------------------- */

@@ -38,8 +38,27 @@ __all__ = [
     "HMatrix", "QkdError", "calculate_syndrome", "sum_product_decoding",
     "sum_product_decoding_irregular", "sum_product_decoding_regular", "qkd_ldpc",
     "QKD_LDPC_irregular", "QKD_LDPC_regular", "keygen", "run_trials", "make_seeds",
-    "qber_range", "Workspace", "counters_to_stats",
+    "qber_range", "Workspace", "counters_to_stats", "decoder_flags",
 ]
+
+
+def decoder_flags(threshold_enabled: bool = True, variant: str = "sp_f64",
+                  minsum_scale: float | None = None) -> int:
+    """Flag word of the decode entry points: the reference's threshold switch
+    (CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD) and the check-node rule:
+    "sp_f64" (the reference, bit-exact), "sp_f32" or "minsum" (build-defined
+    binary32 variants; minsum_scale in (0, 1), a multiple of 1/256)."""
+    if variant not in N.VARIANTS:
+        raise ValueError(f"unknown decoder variant {variant!r}; one of {sorted(N.VARIANTS)}")
+    flags = (FLAG_THRESHOLD if threshold_enabled else 0) | N.VARIANTS[variant]
+    if minsum_scale is not None:
+        if variant != "minsum":
+            raise ValueError("minsum_scale applies to variant='minsum' only")
+        q = round(minsum_scale * 256)
+        if not (1 <= q <= 255) or q != minsum_scale * 256:
+            raise ValueError("minsum_scale must be k/256 for k in 1..255")
+        flags |= q << N.MINSUM_SCALE_SHIFT
+    return flags
 
 
 def _ptr(t) -> int | None:
@@ -195,7 +214,8 @@ class LDPCResult:
 
 def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
                          msg_threshold: float = 100.0, threshold_enabled: bool = True,
-                         want_bits: bool = True, workspace=None, stream=None) -> SPResult:
+                         want_bits: bool = True, workspace=None, stream=None,
+                         variant: str = "sp_f64", minsum_scale: float | None = None) -> SPResult:
     """sum_product_decoding_irregular/_regular (qkd_ldpc_algorithm.cpp:3-345), batched.
     llr [F, N] float64, syndrome [F, M] uint8 (0/1)."""
     _need_cuda(llr, torch.float64, "llr")
@@ -205,7 +225,7 @@ def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
     bits = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev) if want_bits else None
     iters = torch.empty(f, dtype=torch.int32, device=dev)
     ok = torch.empty(f, dtype=torch.uint8, device=dev)
-    flags = FLAG_THRESHOLD if threshold_enabled else 0
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale)
     N.check(N.lib().qkd_decode_batch(H.handle, _ws(workspace), _ptr(llr), _ptr(syndrome), f,
                                      max_iterations, msg_threshold, flags, _ptr(bits), _ptr(iters),
                                      _ptr(ok), _stream(stream)))
@@ -219,7 +239,8 @@ sum_product_decoding_regular = sum_product_decoding
 
 def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
              msg_threshold: float = 100.0, threshold_enabled: bool = True,
-             want_bits: bool = False, workspace=None, stream=None) -> LDPCResult:
+             want_bits: bool = False, workspace=None, stream=None,
+             variant: str = "sp_f64", minsum_scale: float | None = None) -> LDPCResult:
     """QKD_LDPC_irregular/_regular (qkd_ldpc_algorithm.cpp:347-447), batched.
     alice, bob [F, N] uint8 (0/1); one QBER for the batch."""
     _need_cuda(alice, torch.uint8, "alice")
@@ -230,7 +251,7 @@ def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
     iters = torch.empty(f, dtype=torch.int32, device=dev)
     ok = torch.empty(f, dtype=torch.uint8, device=dev)
     km = torch.empty(f, dtype=torch.uint8, device=dev)
-    flags = FLAG_THRESHOLD if threshold_enabled else 0
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale)
     N.check(N.lib().qkd_qkd_ldpc_batch(H.handle, _ws(workspace), _ptr(alice), _ptr(bob), f, qber,
                                        max_iterations, msg_threshold, flags, _ptr(bits),
                                        _ptr(iters), _ptr(ok), _ptr(km), _stream(stream)))
@@ -268,7 +289,8 @@ class TrialResults:
 def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                max_iterations: int = 50, msg_threshold: float = 100.0,
                threshold_enabled: bool = True, workspace=None, stream=None,
-               out: TrialResults | None = None) -> TrialResults:
+               out: TrialResults | None = None, variant: str = "sp_f64",
+               minsum_scale: float | None = None) -> TrialResults:
     """run_trial (simulation.cpp:161-189) for every frame, fused on the device, plus the
     per-QBER-point counters of simulation.cpp:252-312. seeds: int64 CUDA tensor holding
     the uint64 seed bits."""
@@ -281,7 +303,7 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                            torch.empty(f, dtype=torch.uint8, device=dev),
                            torch.empty(f, dtype=torch.float64, device=dev),
                            torch.empty(N.COUNTERS_BYTES, dtype=torch.uint8, device=dev))
-    flags = FLAG_THRESHOLD if threshold_enabled else 0
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale)
     N.check(N.lib().qkd_trials_batch(H.handle, _ws(workspace), _ptr(seeds), seed_offset, f,
                                      q_nominal, max_iterations, msg_threshold, flags,
                                      _ptr(out.iterations), _ptr(out.syndromes_match),

@@ -34,6 +34,10 @@ ERR_IO = 7
 ERR_UNSUPPORTED = 8
 
 FLAG_THRESHOLD = 0x1
+# decoder variants (include/qkd_ldpc.h: QKD_VARIANT_*)
+VARIANTS = {"sp_f64": 0x00, "sp_f32": 0x10, "minsum": 0x20}
+MINSUM_SCALE_SHIFT = 8
+MINSUM_DEFAULT_SCALE = 0.8125
 
 # Every symbol include/qkd_ldpc.h declares (checked by tests/test_abi.py).
 EXPORTS = [

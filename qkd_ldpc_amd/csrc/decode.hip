@@ -45,12 +45,23 @@ enum DecodeMode : int {
     kModeKeys = 1  // QKD_LDPC path: packed alice/bob keys, LLR = +-log_p
 };
 
+// Check-node rule and message width (QKD_VARIANT_* in qkd_ldpc.h).
+//   kRuleSp64   the reference's sum-product in binary64, bit-exact
+//   kRuleSp32   the same schedule with binary32 messages and totals, OCML
+//               tanhf/atanhf (a variant: not bit-exact to anything)
+//   kRuleMinSum normalised min-sum in binary32: c2b = scale * sign * min|b2c|
+//               over the other edges of the check (a variant, no transcendental)
+enum DecodeRule : int { kRuleSp64 = 0, kRuleSp32 = 1, kRuleMinSum = 2 };
+template <int RULE> struct RuleMsg { using T = float; };
+template <> struct RuleMsg<kRuleSp64> { using T = double; };
+
 struct DecodeArgs {
     DeviceCode code;
     uint32_t n_frames;
     uint32_t max_it;
     double thr;
     int clamp_on;
+    float ms_scale;    // kRuleMinSum normalisation
     // kModeLlr
     const double* llr;
     const uint8_t* syn;
@@ -103,7 +114,8 @@ struct PhaseClock {
     }
 };
 
-__device__ __forceinline__ double clamp_msg(double v, double thr) {
+template <typename T>
+__device__ __forceinline__ T clamp_msg(T v, T thr) {
     // threshold_matrix_irregular (array_and_matrix_operations.cpp:508-524):
     // compare-based, so NaN passes through.
     return v > thr ? thr : (v < -thr ? -thr : v);
@@ -127,7 +139,7 @@ __device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) 
 __host__ __device__ inline int decode_m_words(int m) { return ((m + 63) / 64) * 2; }
 
 // LDS layout of decode_kernel (bytes):
-//   total  [n_pad]          binary64 bit totals (the reference's `total`, :256-267)
+//   total  [n_pad]          bit totals (the reference's `total`, :256-267), message width
 //   tsyn   [m_words]        target syndrome, one bit per check
 //   xsyn   [m_words]        syndrome of the current hard decision (XOR-built)
 //   qsyn   [m_words]        QKD path: sign of each check's first-iteration product
@@ -139,15 +151,15 @@ __host__ __device__ inline int decode_m_words(int m) { return ((m + 63) / 64) * 
 //   ctl    [4]              frame index, block_any flags
 struct DecodeLds {
     size_t tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, bytes;
-    __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries) {
+    __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries, int esz) {
         const int m_words = decode_m_words(m);
-        tsyn = (size_t)n_pad * 8;
+        tsyn = ((size_t)n_pad * esz + 15) & ~(size_t)15;
         xsyn = tsyn + (size_t)m_words * 4;
         qsyn = xsyn + (size_t)m_words * 4;
         tval = (qsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
         // the tanh rows double as the prologue's staging area for the frame's
         // Alice and Bob words
-        const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * 8;
+        const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * esz;
         const size_t stage = (size_t)n_words * 16;
         ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
@@ -191,30 +203,85 @@ enum CheckSrc : int {
     kSrcTable = 2      // second QKD iteration: looked up (second_table_index)
 };
 
-template <int SRC, bool CLAMP, int DC>
-__device__ __forceinline__ double check_edge(double x, double old, uint32_t w, uint32_t sbit, int lane,
-                                             double thr, double* row, int min_dc, uint32_t dummy) {
+template <int RULE> struct RuleMath;
+template <> struct RuleMath<kRuleSp64> {
+    static __device__ __forceinline__ double tanh_half(double x) { return qkdm::tanh_flat(x / 2.0); }
+    static __device__ __forceinline__ double two_atanh(double p) { return 2.0 * qkdm::atanh_flat(p); }
+};
+template <> struct RuleMath<kRuleSp32> {
+    static __device__ __forceinline__ float tanh_half(float x) { return tanhf(x * 0.5f); }
+    // In binary32, tanh(b2c / 2) rounds to 1 from |b2c| ~ 18 on, so the
+    // extrinsic ratio P / t lands on (or one ulp beyond) +-1 far more often
+    // than in binary64, and 2 atanh(+-1) = +-inf would turn a ~17 message into
+    // the clamp value. The ratio is therefore limited to the largest binary32
+    // below 1 (|message| <= 2 atanh(1 - 2^-24) = 17.33); NaN (0/0) still passes.
+    static __device__ __forceinline__ float two_atanh(float p) {
+        constexpr float kMax = 0x1.fffffep-1f;
+        p = p > kMax ? kMax : (p < -kMax ? -kMax : p);
+        return 2.0f * atanhf(p);
+    }
+};
+
+template <int SRC, bool CLAMP, int DC, int RULE, typename T>
+__device__ __forceinline__ T check_edge(T x, T old, uint32_t w, uint32_t sbit, int lane, T thr, T* row,
+                                        float ms_scale) {
     if (SRC == kSrcGeneral) {
         x = x - old;
         if (CLAMP) x = clamp_msg(x, thr);
     }
-    const double tv = SRC == kSrcTable ? x : qkdm::tanh_flat(x / 2.0);
-    row[lane] = tv;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int start = pw_start(w);
     const int deg = pw_deg(w);
-    double o[DC];
+    if constexpr (RULE == kRuleMinSum) {
+        // c2b = scale * (s_j ^ signs of the other b2c) * min over the other |b2c|
+        row[lane] = x;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        T o[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) o[k] = row[start + k];
-    double P = sbit ? -1.0 : 1.0;
-    P = P * o[0];                         // every check has degree >= 1
+        for (int k = 0; k < DC; ++k) o[k] = row[start + k];
+        uint32_t neg = sbit ^ (x < 0 ? 1u : 0u);
+        T mn = __builtin_inff();
 #pragma unroll
-    for (int k = 1; k < DC; ++k) P = k < deg ? P * o[k] : P;
-    double v = 2.0 * qkdm::atanh_flat(P / tv);
-    if (CLAMP) v = clamp_msg(v, thr);
-    return v;
+        for (int k = 0; k < DC; ++k) {
+            if (k < deg) {
+                neg ^= o[k] < 0 ? 1u : 0u;
+                if (start + k != lane) mn = fminf(mn, fabsf(o[k]));
+            }
+        }
+        T v = (T)ms_scale * mn;
+        v = neg ? -v : v;
+        if (CLAMP) v = clamp_msg(v, thr);
+        return v;
+    } else {
+        const T tv = SRC == kSrcTable ? x : RuleMath<RULE>::tanh_half(x);
+        row[lane] = tv;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        T o[DC];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) o[k] = row[start + k];
+        T P = sbit ? (T)-1 : (T)1;
+        T v;
+        if constexpr (RULE == kRuleSp64) {
+            // the reference's P = prod_k t_k, then P / t_self (:231-241)
+            P = P * o[0];                     // every check has degree >= 1
+#pragma unroll
+            for (int k = 1; k < DC; ++k) P = k < deg ? P * o[k] : P;
+            v = RuleMath<RULE>::two_atanh(P / tv);
+        } else {
+            // binary32 variant: the extrinsic product over the other edges in
+            // ascending order, no division. (P / t is 0/0 = NaN when b2c is
+            // exactly 0, which binary32 cancellation makes a ~1 % per-frame
+            // event at QBER 0.05, and the NaN then floods the frame.)
+#pragma unroll
+            for (int k = 0; k < DC; ++k) P = (k < deg && start + k != lane) ? P * o[k] : P;
+            v = RuleMath<RULE>::two_atanh(P);
+        }
+        if (CLAMP) v = clamp_msg(v, thr);
+        return v;
+    }
 }
 
 // The check phase of one iteration for one wave: tasks wave, wave+NW, ...
@@ -227,44 +294,44 @@ __device__ __forceinline__ double check_edge(double x, double old, uint32_t w, u
 // for memory operations that had a whole task of arithmetic to complete.
 // The plan is padded with idle tasks (qkd_plan.h): no bounds tests on the
 // look-ahead loads.
-template <int SRC, bool CLAMP, int DC>
+template <int SRC, bool CLAMP, int DC, int RULE, typename T>
 __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
-                                            const double* total, const uint16_t* t2idx, const double* tab2,
-                                            double* __restrict__ c2b, double* row,
-                                            int n_tasks, int n_pad, double thr, int wave, int lane,
-                                            int min_dc, uint32_t dummy) {
+                                            const T* total, const uint16_t* t2idx, const double* tab2,
+                                            T* __restrict__ c2b, T* row, int n_tasks, int n_pad, T thr,
+                                            int wave, int lane, float ms_scale) {
     constexpr int NW = kDecodeBlock / 64;
     constexpr bool FIRST = SRC != kSrcGeneral;    // no stored message is read
     int t = wave;
     if (t >= n_tasks) return;
     const uint2* pl = plan + lane;
-    auto msg = [&](uint2 p) -> double* { return c2b + pw_row(p.x) * n_pad + pw_bit(p.x); };
+    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + pw_bit(p.x); };
     // the incoming value: a bit total, or (kSrcTable) the tabulated tanh
-    auto src = [&](uint2 p) -> double {
-        return SRC == kSrcTable ? tab2[t2idx[pw_bit(p.x)] + pw_row(p.x)] : total[pw_bit(p.x)];
+    auto src = [&](uint2 p) -> T {
+        if constexpr (SRC == kSrcTable) return tab2[t2idx[pw_bit(p.x)] + pw_row(p.x)];
+        else return total[pw_bit(p.x)];
     };
     // the target syndrome bit of the lane's check
     auto sbit = [&](uint2 p) -> uint32_t { return (tsyn[p.y >> 5] >> (p.y & 31)) & 1u; };
     uint2 wa = pl[t * 64];
     uint2 wb = pl[(t + NW) * 64];
-    double xa = src(wa);
-    double oa = FIRST ? 0.0 : *msg(wa);
-    double* pend = nullptr;      // message computed by the previous task, not yet stored
-    double pv = 0.0;
+    T xa = src(wa);
+    T oa = FIRST ? (T)0 : *msg(wa);
+    T* pend = nullptr;      // message computed by the previous task, not yet stored
+    T pv = 0;
     for (;;) {
         if (pend) *pend = pv;
         const uint2 wc = pl[(t + 2 * NW) * 64];
-        const double xb = src(wb);
-        const double ob = FIRST ? 0.0 : *msg(wb);
-        pv = check_edge<SRC, CLAMP, DC>(xa, oa, wa.x, sbit(wa), lane, thr, row, min_dc, dummy);
+        const T xb = src(wb);
+        const T ob = FIRST ? (T)0 : *msg(wb);
+        pv = check_edge<SRC, CLAMP, DC, RULE>(xa, oa, wa.x, sbit(wa), lane, thr, row, ms_scale);
         pend = msg(wa);
         t += NW;
         if (t >= n_tasks) break;
         *pend = pv;
         wa = pl[(t + 2 * NW) * 64];
         xa = src(wc);
-        oa = FIRST ? 0.0 : *msg(wc);
-        pv = check_edge<SRC, CLAMP, DC>(xb, ob, wb.x, sbit(wb), lane, thr, row, min_dc, dummy);
+        oa = FIRST ? (T)0 : *msg(wc);
+        pv = check_edge<SRC, CLAMP, DC, RULE>(xb, ob, wb.x, sbit(wb), lane, thr, row, ms_scale);
         pend = msg(wb);
         t += NW;
         if (t >= n_tasks) break;
@@ -378,19 +445,23 @@ __device__ __forceinline__ void first_check_phase(const uint2* __restrict__ plan
 //    hard decision z_i = total_i <= 0; if z_i, XOR it into the syndrome bit of
 //    each of its checks (LDS bit array; XOR is order-free, so exact)
 //  syndrome test (:277-285): compare with the target words, block-wide any()
-template <int MODE, int DC, bool CLAMP>
+template <int MODE, int RULE, int DC, bool CLAMP>
 __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
+    using T = typename RuleMsg<RULE>::T;
+    // the exact QKD-path shortcuts (first/second-iteration tables) exist for
+    // the reference rule only
+    constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
-    const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries);
+    const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries, (int)sizeof(T));
     const int m_words = decode_m_words(c.m);
-    double* total = reinterpret_cast<double*>(smem);
+    T* total = reinterpret_cast<T*>(smem);
     uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
     uint32_t* qsyn = reinterpret_cast<uint32_t*>(smem + L.qsyn);
     // QKD path with both tables: the first check phase is folded into the
     // first bit phase (fold_first_message)
-    const bool fold1 = MODE == kModeKeys && a.first_table && a.tab2_entries;
+    const bool fold1 = TABLES && a.first_table && a.tab2_entries;
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;     // sign bit of log_p
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
@@ -399,18 +470,19 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    double* row = reinterpret_cast<double*>(smem + L.tval) + wave * (64 + DC);
+    T* row = reinterpret_cast<T*>(smem + L.tval) + wave * (64 + DC);
     const int n_tasks = c.n_tasks;
     const int n_pad = c.n_pad;
     const uint2* plan = c.plan;
-    double* c2b = a.c2b + (size_t)blockIdx.x * a.c2b_stride;
-    const double thr = a.thr;
+    T* c2b = reinterpret_cast<T*>(a.c2b + (size_t)blockIdx.x * a.c2b_stride);
+    const T thr = (T)a.thr;
+    const T llr_p = (T)a.log_p;
     uint32_t any_k = 0;
     if (tid == 0) { ctl[2] = 0; ctl[3] = 0; }
-    if (MODE == kModeKeys && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
-    if (MODE == kModeKeys && a.tab2_entries) {
+    if (TABLES && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
+    if (TABLES && a.tab2_entries) {
         __syncthreads();
-        second_table_fill<CLAMP>(c, ctab, a.log_p, thr, tab2, a.tab2_entries);
+        second_table_fill<CLAMP>(c, ctab, a.log_p, a.thr, tab2, a.tab2_entries);
     }
     PhaseClock pc(a.phase);
 
@@ -439,17 +511,17 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         {
             int r = 0;
             for (int i = tid; i < c.n; i += kDecodeBlock, ++r) {
-                double l;
+                T l;
                 if (MODE == kModeLlr) {
-                    l = a.llr[(size_t)f * c.n + i];
+                    l = (T)a.llr[(size_t)f * c.n + i];
                 } else {
                     const uint32_t bb = (uint32_t)((sw[a.words + (i >> 6)] >> (i & 63)) & 1u);
                     bobmask |= bb << r;
-                    l = bb ? -a.log_p : a.log_p;
+                    l = bb ? -llr_p : llr_p;
                 }
                 total[i] = l;
             }
-            if (tid == 0) total[c.n] = 0.0;
+            if (tid == 0) total[c.n] = 0;
         }
         // ---- prologue: target syndrome bits per check (tsyn) and, on the QKD
         //      path, each check's first-product sign (qsyn, fold_first_message);
@@ -506,27 +578,35 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         bool done = false;
         uint32_t it = 0;
         for (; it < a.max_it; ++it) {
-            if (it == 0 && fold1)
-                ;   // messages rebuilt from signs in the bit phase (fold_first_message)
-            else if (it == 0 && MODE == kModeKeys && a.first_table)
-                first_check_phase(plan, tsyn, total, ctab, c2b, n_tasks, n_pad, wave, lane);
-            else if (it == 0)
-                check_phase<kSrcFirst, CLAMP, DC>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
-                                                  thr, wave, lane, c.min_dc, (uint32_t)c.n);
-            else if (it == 1 && MODE == kModeKeys && a.tab2_entries)
-                check_phase<kSrcTable, CLAMP, DC>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
-                                                  thr, wave, lane, c.min_dc, (uint32_t)c.n);
-            else
-                check_phase<kSrcGeneral, CLAMP, DC>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks, n_pad,
-                                                    thr, wave, lane, c.min_dc, (uint32_t)c.n);
+            bool tabled = false;
+            if constexpr (TABLES) {
+                tabled = true;
+                if (it == 0 && fold1)
+                    ;   // messages rebuilt from signs in the bit phase (fold_first_message)
+                else if (it == 0 && a.first_table)
+                    first_check_phase(plan, tsyn, total, ctab, c2b, n_tasks, n_pad, wave, lane);
+                else if (it == 1 && a.tab2_entries)
+                    check_phase<kSrcTable, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks,
+                                                            n_pad, thr, wave, lane, a.ms_scale);
+                else
+                    tabled = false;
+            }
+            if (!tabled) {
+                if (it == 0)
+                    check_phase<kSrcFirst, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks,
+                                                            n_pad, thr, wave, lane, a.ms_scale);
+                else
+                    check_phase<kSrcGeneral, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks,
+                                                              n_pad, thr, wave, lane, a.ms_scale);
+            }
             __syncthreads();
-            pc.mark((MODE == kModeKeys && it < 2 && a.first_table) ? 5 + (int)it : 1);
+            pc.mark((TABLES && it < 2 && a.first_table) ? 5 + (int)it : 1);
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
             // and the hard decision's syndrome (:277, calculate_syndrome_irregular :476-486).
             // kBitChunk rounds at a time: all their message rows and check indices
             // are loaded before any of them is summed.
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kBitChunk) {
-                double v[kBitChunk][kDvUnroll];
+                T v[kBitChunk][kDvUnroll];
                 int32_t jc[kBitChunk][kDvUnroll];
                 int dg[kBitChunk];
 #pragma unroll
@@ -537,7 +617,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k) {
                         const bool ld = ok && k < c.max_dv;
-                        v[u][k] = (ld && !(fold1 && it == 0)) ? c2b[k * n_pad + i] : 0.0;
+                        v[u][k] = (ld && !(fold1 && it == 0)) ? c2b[k * n_pad + i] : (T)0;
                         jc[u][k] = ld ? c.bit_chk[k * n_pad + i] : 0;
                     }
                 }
@@ -547,10 +627,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     const int i = tid + r * kDecodeBlock;
                     if (i >= c.n) break;
                     const int deg = dg[u];
-                    double acc;
-                    if (MODE == kModeLlr) acc = a.llr[(size_t)f * c.n + i];
-                    else acc = ((bobmask >> r) & 1u) ? -a.log_p : a.log_p;
-                    if (MODE == kModeKeys && fold1 && it == 0) {
+                    T acc;
+                    if (MODE == kModeLlr) acc = (T)a.llr[(size_t)f * c.n + i];
+                    else acc = ((bobmask >> r) & 1u) ? -llr_p : llr_p;
+                    if constexpr (TABLES) if (fold1 && it == 0) {
                         // fold_first_message: message of the k-th check j of bit i is
                         // +-C_{d_j} with sign = sign(P_j) ^ sign(LLR_i) (first_check_phase)
                         const uint32_t sgi = ((bobmask >> r) & 1u) ^ lsign;
@@ -569,7 +649,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
                     for (int k = kDvUnroll; k < deg; ++k) acc = acc + c2b[k * n_pad + i];
                     total[i] = acc;
-                    if (MODE == kModeKeys && a.tab2_entries && it == 0) {
+                    if constexpr (TABLES) if (a.tab2_entries && it == 0) {
                         // second_table_index: bob bit and the signs of the first messages
                         uint32_t code = (bobmask >> r) & 1u;
 #pragma unroll
@@ -577,7 +657,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                             if (k < deg) code |= ((uint32_t)qkdm::hi32(v[u][k]) >> 31) << (1 + k);
                         t2idx[i] = (uint16_t)(c.bit_pat[i] * tab2_stride(c.max_dv) + code * c.max_dv);
                     }
-                    if (acc <= 0.0) {
+                    if (acc <= 0) {
 #pragma unroll
                         for (int k = 0; k < kDvUnroll; ++k)
                             if (k < deg) atomicXor(&xsyn[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
@@ -607,7 +687,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         // ---- outputs: SP_result + last hard decision (+ keys_match)
         bool key_mismatch = false;
         for (int i = tid; i < c.n; i += kDecodeBlock) {
-            const uint8_t d = total[i] <= 0.0 ? 1 : 0;
+            const uint8_t d = total[i] <= 0 ? 1 : 0;
             if (a.bits_out) a.bits_out[(size_t)f * c.n + i] = d;
             if (MODE == kModeKeys) {
                 const uint64_t w = a.alice_w[(size_t)f * a.words + (i >> 6)];
@@ -887,24 +967,48 @@ __global__ void counters_init_kernel(qkd_counters* c) {
 using DecodeFn = void (*)(DecodeArgs);
 
 // Check-degree buckets: the in-check product reads DC values per lane.
-template <int MODE, bool CLAMP>
+template <int MODE, int RULE, bool CLAMP>
 static DecodeFn pick_decode_dc(int max_dc, int* dc) {
-    if (max_dc <= 4) { *dc = 4; return decode_kernel<MODE, 4, CLAMP>; }
-    if (max_dc <= 6) { *dc = 6; return decode_kernel<MODE, 6, CLAMP>; }
-    if (max_dc <= 8) { *dc = 8; return decode_kernel<MODE, 8, CLAMP>; }
-    if (max_dc <= 16) { *dc = 16; return decode_kernel<MODE, 16, CLAMP>; }
+    if (max_dc <= 4) { *dc = 4; return decode_kernel<MODE, RULE, 4, CLAMP>; }
+    if (max_dc <= 6) { *dc = 6; return decode_kernel<MODE, RULE, 6, CLAMP>; }
+    if (max_dc <= 8) { *dc = 8; return decode_kernel<MODE, RULE, 8, CLAMP>; }
+    if (max_dc <= 16) { *dc = 16; return decode_kernel<MODE, RULE, 16, CLAMP>; }
     *dc = 64;
-    return decode_kernel<MODE, 64, CLAMP>;
+    return decode_kernel<MODE, RULE, 64, CLAMP>;
 }
 
-static DecodeFn pick_decode(int mode, bool clamp, int max_dc, int* dc) {
-    if (mode == kModeLlr)
-        return clamp ? pick_decode_dc<kModeLlr, true>(max_dc, dc) : pick_decode_dc<kModeLlr, false>(max_dc, dc);
-    return clamp ? pick_decode_dc<kModeKeys, true>(max_dc, dc) : pick_decode_dc<kModeKeys, false>(max_dc, dc);
+template <int MODE, int RULE>
+static DecodeFn pick_decode_clamp(bool clamp, int max_dc, int* dc) {
+    return clamp ? pick_decode_dc<MODE, RULE, true>(max_dc, dc) : pick_decode_dc<MODE, RULE, false>(max_dc, dc);
 }
 
-static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries) {
-    return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries).bytes;
+template <int MODE>
+static DecodeFn pick_decode_rule(int rule, bool clamp, int max_dc, int* dc) {
+    if (rule == kRuleSp32) return pick_decode_clamp<MODE, kRuleSp32>(clamp, max_dc, dc);
+    if (rule == kRuleMinSum) return pick_decode_clamp<MODE, kRuleMinSum>(clamp, max_dc, dc);
+    return pick_decode_clamp<MODE, kRuleSp64>(clamp, max_dc, dc);
+}
+
+static DecodeFn pick_decode(int mode, int rule, bool clamp, int max_dc, int* dc) {
+    return mode == kModeLlr ? pick_decode_rule<kModeLlr>(rule, clamp, max_dc, dc)
+                            : pick_decode_rule<kModeKeys>(rule, clamp, max_dc, dc);
+}
+
+static int rule_of(uint32_t flags) {
+    switch (flags & QKD_VARIANT_MASK) {
+        case QKD_VARIANT_SP_F32: return kRuleSp32;
+        case QKD_VARIANT_MINSUM: return kRuleMinSum;
+        default: return kRuleSp64;
+    }
+}
+
+static float minsum_scale_of(uint32_t flags) {
+    const uint32_t q = (flags >> QKD_MINSUM_SCALE_SHIFT) & 0xffu;
+    return q ? (float)q / 256.0f : (float)QKD_MINSUM_DEFAULT_SCALE;
+}
+
+static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries, int rule) {
+    return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries, rule == kRuleSp64 ? 8 : 4).bytes;
 }
 
 // Resident workgroups of decode_kernel for this code on its device.
@@ -996,10 +1100,12 @@ struct WsSession {
 static unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs& a, int mode,
-                                hipStream_t stream) {
+                                uint32_t flags, hipStream_t stream) {
     int dc = 0;
-    DecodeFn fn = pick_decode(mode, a.clamp_on != 0, c->max_dc, &dc);
-    const size_t lds = decode_lds_bytes(c, dc, a.tab2_entries);
+    const int rule = rule_of(flags);
+    a.ms_scale = minsum_scale_of(flags);
+    DecodeFn fn = pick_decode(mode, rule, a.clamp_on != 0, c->max_dc, &dc);
+    const size_t lds = decode_lds_bytes(c, dc, a.tab2_entries, rule);
     int grid = 0;
     qkd_status s = decode_grid(c, fn, lds, &grid);
     if (s != QKD_OK) return s;
@@ -1030,7 +1136,12 @@ static qkd_status check_frames(size_t n_frames) {
 
 static qkd_status check_decode_params(uint32_t max_it, double thr, uint32_t flags) {
     if (max_it < 1) return set_error(QKD_ERR_INVALID_ARG, "max_iterations must be >= 1");
-    if (flags & ~QKD_FLAG_THRESHOLD) return set_error(QKD_ERR_INVALID_ARG, "unknown flags 0x%x", flags);
+    const uint32_t known = QKD_FLAG_THRESHOLD | QKD_VARIANT_MASK | (0xffu << QKD_MINSUM_SCALE_SHIFT);
+    if (flags & ~known) return set_error(QKD_ERR_INVALID_ARG, "unknown flags 0x%x", flags);
+    if ((flags & QKD_VARIANT_MASK) == QKD_VARIANT_MASK)
+        return set_error(QKD_ERR_INVALID_ARG, "unknown decoder variant 0x%x", flags & QKD_VARIANT_MASK);
+    if ((flags >> QKD_MINSUM_SCALE_SHIFT) && (flags & QKD_VARIANT_MASK) != QKD_VARIANT_MINSUM)
+        return set_error(QKD_ERR_INVALID_ARG, "min-sum scale given without QKD_VARIANT_MINSUM");
     if ((flags & QKD_FLAG_THRESHOLD) && !(thr > 0.0))
         return set_error(QKD_ERR_INVALID_ARG, "message threshold must be > 0");
     return QKD_OK;
@@ -1103,7 +1214,7 @@ qkd_status qkd_decode_batch(const qkd_code* c, qkd_workspace* ws, const double* 
     a.bits_out = bits_out;
     a.iters = iterations;
     a.sp_ok = syndromes_match;
-    return launch_decode(c, ws, a, kModeLlr, (hipStream_t)stream);
+    return launch_decode(c, ws, a, kModeLlr, flags, (hipStream_t)stream);
 }
 
 // Shared by qkd_qkd_ldpc_batch and qkd_trials_batch: keys already packed in ws.
@@ -1120,7 +1231,7 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     a.words = (uint32_t)((c->n + 63) / 64);
     a.log_p = std::log((1. - q) / q);          // host glibc log, qkd_ldpc_algorithm.cpp:400
     // first-iteration message magnitudes by check degree (first_check_phase)
-    a.first_table = c->max_dc <= kFirstTableDeg ? 1 : 0;
+    a.first_table = (c->max_dc <= kFirstTableDeg && rule_of(flags) == kRuleSp64) ? 1 : 0;
     if (a.first_table) {
         const double T = std::fabs(qkdm::tanh_flat(a.log_p / 2.0));
         double M = 1.0;
@@ -1137,7 +1248,7 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     a.iters = iters;
     a.sp_ok = sp_ok;
     a.key_ok = key_ok;
-    return launch_decode(c, ws, a, kModeKeys, stream);
+    return launch_decode(c, ws, a, kModeKeys, flags, stream);
 }
 
 qkd_status qkd_qkd_ldpc_batch(const qkd_code* c, qkd_workspace* ws, const uint8_t* alice,
@@ -1223,12 +1334,18 @@ qkd_status qkd_keygen_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t
 
 __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) y[i] = which == 0 ? qkdm::tanh_flat(x[i]) : qkdm::atanh_flat(x[i]);
+    if (i >= n) return;
+    switch (which) {
+        case 0: y[i] = qkdm::tanh_flat(x[i]); break;
+        case 1: y[i] = qkdm::atanh_flat(x[i]); break;
+        case 2: y[i] = (double)RuleMath<kRuleSp32>::tanh_half((float)x[i]); break;
+        default: y[i] = (double)RuleMath<kRuleSp32>::two_atanh((float)x[i]); break;
+    }
 }
 
 qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void* stream) {
     clear_error();
-    if (!x || !y || (which != 0 && which != 1)) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if (!x || !y || which < 0 || which > 3) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
     if (n == 0) return QKD_OK;
     hipLaunchKernelGGL(math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, which,
                        x, y, n);

@@ -1,0 +1,223 @@
+"""Decoder variants (include/qkd_ldpc.h QKD_VARIANT_*).
+
+The reference has one decoder, binary64 sum-product; that is QKD_VARIANT_SP_F64
+and the parity suites (test_gpu_parity.py) hold it to the reference bit for bit.
+The variants are build-defined:
+  * min-sum: checked bit for bit against its numpy binary32 specification
+    (oracle/variants.py) - decoded words, iteration counts, flags;
+  * binary32 sum-product: checked bit for bit against its numpy specification
+    with the device's own elementwise tanhf/atanhf plugged in (OCML has no
+    bit-exact CPU twin here; those two functions are checked separately against
+    numpy's float32 ones to ~1 ulp), and against the reference decoder's outcome
+    where the code has margin.
+Frame error rates of both against the reference curve are reported by bench.py.
+"""
+import numpy as np
+import pytest
+
+from oracle.variants import MinSumModel
+
+
+@pytest.fixture(scope="module")
+def ms_model(golden_code):
+    return MinSumModel(int(golden_code["dims"][0]), int(golden_code["dims"][1]),
+                       golden_code["chk_off"], golden_code["chk_idx"])
+
+
+def _frames(oracle_mod, q, count, seed=777):
+    A, B = [], []
+    for s in oracle_mod.seeds(seed, count):
+        a, b, qq = oracle_mod.keygen(int(s), 10240, q)
+        A.append(a)
+        B.append(b)
+    return np.array(A, np.uint8), np.array(B, np.uint8), qq
+
+
+# ---- CPU: the specification itself ------------------------------------------------
+
+def test_minsum_model_decodes_low_qber(ms_model, oracle_mod):
+    A, B, q = _frames(oracle_mod, 0.03, 8)
+    lp = np.log((1 - q) / q)
+    llr = np.where(B == 1, -lp, lp)
+    bits, it, ok = ms_model.decode(llr, ms_model.syndrome(A))
+    assert ok.all() and (bits == A).all()
+    assert (it >= 2).all() and (it <= 10).all()
+
+
+def test_minsum_model_syndrome_matches_oracle(ms_model, oracle_code):
+    rng = np.random.default_rng(5)
+    bits = rng.integers(0, 2, (3, 10240)).astype(np.uint8)
+    got = ms_model.syndrome(bits)
+    for f in range(3):
+        assert (got[f] == oracle_code.syndrome(bits[f])).all()
+
+
+def test_decoder_flags_validation():
+    import qkd_ldpc_amd as Q
+    assert Q.decoder_flags(True, "sp_f64") == 0x1
+    assert Q.decoder_flags(False, "minsum") == 0x20
+    assert Q.decoder_flags(True, "minsum", 0.5) == 0x1 | 0x20 | (128 << 8)
+    with pytest.raises(ValueError):
+        Q.decoder_flags(True, "bogus")
+    with pytest.raises(ValueError):
+        Q.decoder_flags(True, "sp_f32", 0.5)
+    with pytest.raises(ValueError):
+        Q.decoder_flags(True, "minsum", 0.3)     # not k/256
+
+
+# ---- GPU ---------------------------------------------------------------------------
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def Q():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import qkd_ldpc_amd as Q
+    return Q
+
+
+@pytest.fixture(scope="module")
+def H(Q, golden_code):
+    return Q.HMatrix.from_check_lists(int(golden_code["dims"][0]), golden_code["chk_off"],
+                                      golden_code["chk_idx"])
+
+
+def _dev(x, dtype):
+    return torch.from_numpy(np.ascontiguousarray(x).astype(dtype)).cuda()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,max_it,thr,thr_on,scale", [
+    (0.02, 50, 100.0, True, None),
+    (0.06, 50, 100.0, True, None),
+    (0.08, 50, 100.0, True, 0.8125),
+    (0.08, 7, 2.5, True, 0.5),
+    (0.05, 50, 0.0, False, None),
+    (0.10, 3, 0.7, True, 255 / 256),
+])
+def test_minsum_llr_bit_exact(Q, H, ms_model, oracle_mod, q, max_it, thr, thr_on, scale):
+    A, B, qq = _frames(oracle_mod, q, 48, seed=int(q * 1000) + max_it)
+    lp = np.log((1 - qq) / qq)
+    llr = np.where(B == 1, -lp, lp)
+    syn = ms_model.syndrome(A)
+    r = Q.sum_product_decoding(H, _dev(llr, np.float64), _dev(syn, np.uint8), max_it,
+                               thr if thr_on else 100.0, thr_on, variant="minsum",
+                               minsum_scale=scale)
+    torch.cuda.synchronize()
+    want_bits, want_it, want_ok = ms_model.decode(llr, syn, max_it, thr, thr_on,
+                                                  0.8125 if scale is None else scale)
+    assert (r.iterations.cpu().numpy() == want_it).all()
+    assert (r.syndromes_match.cpu().numpy() == want_ok).all()
+    assert (r.bits.cpu().numpy() == want_bits).all()
+
+
+@pytest.mark.gpu
+def test_minsum_keys_path_bit_exact(Q, H, ms_model, oracle_mod):
+    """qkd_ldpc (packed-key path, LLR = +-float(log_p)) equals the specification."""
+    A, B, qq = _frames(oracle_mod, 0.07, 48, seed=4242)
+    r = Q.qkd_ldpc(H, _dev(A, np.uint8), _dev(B, np.uint8), float(qq), 50, 100.0, True,
+                   want_bits=True, variant="minsum")
+    torch.cuda.synchronize()
+    lp = np.log((1 - qq) / qq)
+    llr = np.where(B == 1, -lp, lp)
+    want_bits, want_it, want_ok = ms_model.decode(llr, ms_model.syndrome(A), scale=0.8125)
+    assert (r.iterations.cpu().numpy() == want_it).all()
+    assert (r.syndromes_match.cpu().numpy() == want_ok).all()
+    assert (r.bits.cpu().numpy() == want_bits).all()
+    assert (r.keys_match.cpu().numpy() == (want_bits == A).all(axis=1)).all()
+
+
+@pytest.mark.gpu
+def test_minsum_small_codes_bit_exact(Q, dense_codes):
+    rng = np.random.default_rng(17)
+    for name, dense in dense_codes.items():
+        m, n = dense.shape
+        co = np.concatenate([[0], np.cumsum(dense.sum(axis=1))]).astype(np.int32)
+        ci = np.concatenate([np.nonzero(r)[0] for r in dense]).astype(np.int32)
+        model = MinSumModel(n, m, co, ci)
+        Hs = Q.HMatrix.from_dense_array(dense)
+        llr = rng.normal(0.8, 1.5, (16, n))
+        syn = rng.integers(0, 2, (16, m)).astype(np.uint8)
+        r = Q.sum_product_decoding(Hs, _dev(llr, np.float64), _dev(syn, np.uint8), 20, 3.0, True,
+                                   variant="minsum")
+        torch.cuda.synchronize()
+        wb, wi, wo = model.decode(llr, syn, 20, 3.0, True, 0.8125)
+        assert (r.iterations.cpu().numpy() == wi).all(), name
+        assert (r.syndromes_match.cpu().numpy() == wo).all(), name
+        assert (r.bits.cpu().numpy() == wb).all(), name
+
+
+def _dev_math(which):
+    from qkd_ldpc_amd import _native as N
+
+    def f(v):
+        x = torch.from_numpy(np.ascontiguousarray(v, np.float64).ravel()).cuda()
+        y = torch.empty_like(x)
+        N.check(N.lib().qkd_debug_math(which, x.data_ptr(), y.data_ptr(), x.numel(), None))
+        torch.cuda.synchronize()
+        return y.cpu().numpy().astype(np.float32).reshape(np.shape(v))
+    return f
+
+
+@pytest.mark.gpu
+def test_sp_f32_elementwise_math_close_to_numpy(Q):
+    from qkd_ldpc_amd import _native as N
+    x = np.concatenate([np.linspace(-100, 100, 20001), np.linspace(-1, 1, 20001), [0.0, -0.0, 1.0, -1.0]])
+    kmax = np.float32(np.nextafter(np.float32(1), np.float32(0)))
+    with np.errstate(all="ignore"):
+        th = _dev_math(2)(x)
+        at = _dev_math(3)(x)
+        want_th = np.tanh(x.astype(np.float32) * np.float32(0.5))
+        want_at = np.float32(2) * np.arctanh(np.clip(x.astype(np.float32), -kmax, kmax))
+    assert np.allclose(th, want_th, rtol=4e-7, atol=0)
+    assert np.allclose(at, want_at, rtol=4e-7, atol=0)
+    assert np.abs(at).max() <= np.float32(17.33)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,max_it,thr,thr_on", [(0.05, 50, 100.0, True), (0.08, 50, 100.0, True),
+                                                 (0.07, 9, 3.0, True), (0.06, 50, 0.0, False)])
+def test_sp_f32_bit_exact_with_device_math(Q, H, ms_model, oracle_mod, q, max_it, thr, thr_on):
+    from oracle.variants import sp_f32_decode
+    A, B, qq = _frames(oracle_mod, q, 24, seed=int(q * 1000) + 7)
+    lp = np.log((1 - qq) / qq)
+    llr = np.where(B == 1, -lp, lp)
+    syn = ms_model.syndrome(A)
+    r = Q.sum_product_decoding(H, _dev(llr, np.float64), _dev(syn, np.uint8), max_it,
+                               thr if thr_on else 100.0, thr_on, variant="sp_f32")
+    torch.cuda.synchronize()
+    wb, wi, wo = sp_f32_decode(ms_model, llr, syn, max_it, thr, thr_on,
+                               tanh_half=_dev_math(2), two_atanh=_dev_math(3))
+    assert (r.iterations.cpu().numpy() == wi).all()
+    assert (r.syndromes_match.cpu().numpy() == wo).all()
+    assert (r.bits.cpu().numpy() == wb).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [0.02, 0.05])
+def test_sp_f32_tracks_reference(Q, H, q):
+    """binary32 sum-product: where the code has margin it decodes every frame,
+    and to the same iteration count as the reference decoder on nearly all."""
+    seeds = torch.from_numpy(Q.make_seeds(777, 1024).view(np.int64)).cuda()
+    ref = Q.run_trials(H, seeds, q)
+    f32 = Q.run_trials(H, seeds, q, variant="sp_f32")
+    torch.cuda.synchronize()
+    assert f32.syndromes_match.cpu().numpy().all() and f32.keys_match.cpu().numpy().all()
+    same = (ref.iterations.cpu().numpy() == f32.iterations.cpu().numpy()).mean()
+    assert same >= 0.97, same
+
+
+@pytest.mark.gpu
+def test_variant_trials_counters(Q, H):
+    """The fused trial path with a variant: counters agree with the per-frame outputs."""
+    seeds = torch.from_numpy(Q.make_seeds(777, 512).view(np.int64)).cuda()
+    r = Q.run_trials(H, seeds, 0.06, variant="minsum")
+    torch.cuda.synchronize()
+    c = Q.read_counters(r.counters)
+    it = r.iterations.cpu().numpy().astype(np.int64)
+    sp = r.syndromes_match.cpu().numpy().astype(bool)
+    ko = r.keys_match.cpu().numpy().astype(bool)
+    assert c.frames == 512 and c.sp_ok == sp.sum() and c.ldpc_ok == (sp & ko).sum()
+    assert c.sum_iters == it[sp].sum()
