@@ -20,7 +20,8 @@ except Exception:  # pragma: no cover - torch is present in this image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libqkd_ldpc_amd.so")
+# QKD_AMD_LIB points at another build of the same library (diagnostic builds)
+LIB_PATH = os.environ.get("QKD_AMD_LIB") or os.path.join(_HERE, "lib", "libqkd_ldpc_amd.so")
 
 # qkd_status
 OK = 0

@@ -35,10 +35,17 @@
 #include "qkd_plan.h"
 #include "qkd_rng.h"
 
+// Diagnostic builds only (tools/exp_run.sh; never the shipped library): the
+// QKD_EXP_NO_STOP / QKD_EXP_NO_MATH / QKD_EXP_MSG_LOCAL macros run a fixed
+// iteration count / drop the tanh-atanh arithmetic / make the check phase's
+// message accesses coalesced, to split the kernel's time between arithmetic
+// and memory. Results of such builds are wrong by design.
+
 namespace qkd {
 
 // Largest check degree the first-iteration table covers.
 constexpr int kFirstTableDeg = 16;
+
 
 enum DecodeMode : int {
     kModeLlr = 0,  // qkd_decode_batch: caller LLRs + syndrome bytes
@@ -93,10 +100,11 @@ struct DecodeArgs {
     unsigned long long* phase;
 };
 
-// Phase-clock accumulation (diagnostic; a wave-uniform test when off).
+// Phase-clock accumulation (diagnostic; a wave-uniform test when off). Each
+// mark adds straight to the global slot, so nothing is indexed dynamically in
+// registers (an accumulator array would live in scratch).
 struct PhaseClock {
     unsigned long long* out;
-    unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
     long long t = 0;
     __device__ explicit PhaseClock(unsigned long long* o) : out(threadIdx.x == 0 ? o : nullptr) {
         if (out) t = clock64();
@@ -104,14 +112,11 @@ struct PhaseClock {
     __device__ __forceinline__ void mark(int k) {
         if (out) {
             const long long n = clock64();
-            acc[k] += (unsigned long long)(n - t);
+            atomicAdd(out + k, (unsigned long long)(n - t));
             t = n;
         }
     }
-    __device__ void flush() {
-        if (out)
-            for (int k = 0; k < 7; ++k) atomicAdd(out + k, acc[k]);
-    }
+    __device__ void flush() {}
 };
 
 template <typename T>
@@ -222,25 +227,43 @@ template <> struct RuleMath<kRuleSp32> {
     }
 };
 
-template <int SRC, bool CLAMP, int DC, int RULE, typename T>
-__device__ __forceinline__ T check_edge(T x, T old, uint32_t w, uint32_t sbit, int lane, T thr, T* row,
-                                        float ms_scale) {
+// Makes this wave's LDS row writes visible to its own lanes (no s_barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// First half of an edge: the value the lane publishes in its wave's LDS row.
+//   sum-product: t = tanh(b2c / 2) (or the tabulated t), min-sum: b2c itself.
+template <int SRC, bool CLAMP, int RULE, typename T>
+__device__ __forceinline__ T edge_in(T x, T old, T thr) {
     if (SRC == kSrcGeneral) {
         x = x - old;
         if (CLAMP) x = clamp_msg(x, thr);
     }
+#ifdef QKD_EXP_NO_MATH
+    return x * (T)0.5;
+#endif
+    if constexpr (RULE == kRuleMinSum) return x;
+    else return SRC == kSrcTable ? x : RuleMath<RULE>::tanh_half(x);
+}
+
+// Second half: the lane's message from the published row of its check
+// (segment [start, start + deg) of `row`; the row has 64 + DC entries, so reads
+// past a segment's end stay inside it and are discarded).
+template <bool CLAMP, int DC, int RULE, typename T>
+__device__ __forceinline__ T edge_out(T tv, uint32_t w, uint32_t sbit, int lane, T thr, const T* row,
+                                      float ms_scale) {
     const int start = pw_start(w);
     const int deg = pw_deg(w);
+    T o[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) o[k] = row[start + k];
+    T v;
     if constexpr (RULE == kRuleMinSum) {
         // c2b = scale * (s_j ^ signs of the other b2c) * min over the other |b2c|
-        row[lane] = x;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        T o[DC];
-#pragma unroll
-        for (int k = 0; k < DC; ++k) o[k] = row[start + k];
-        uint32_t neg = sbit ^ (x < 0 ? 1u : 0u);
+        uint32_t neg = sbit ^ (tv < 0 ? 1u : 0u);
         T mn = __builtin_inff();
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
@@ -249,42 +272,39 @@ __device__ __forceinline__ T check_edge(T x, T old, uint32_t w, uint32_t sbit, i
                 if (start + k != lane) mn = fminf(mn, fabsf(o[k]));
             }
         }
-        T v = (T)ms_scale * mn;
+        v = (T)ms_scale * mn;
         v = neg ? -v : v;
-        if (CLAMP) v = clamp_msg(v, thr);
-        return v;
-    } else {
-        const T tv = SRC == kSrcTable ? x : RuleMath<RULE>::tanh_half(x);
-        row[lane] = tv;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        T o[DC];
-#pragma unroll
-        for (int k = 0; k < DC; ++k) o[k] = row[start + k];
+    } else if constexpr (RULE == kRuleSp64) {
+        // the reference's P = (s_j ? -1 : 1) * prod_k t_k, then 2 atanh(P / t_self) (:231-241)
         T P = sbit ? (T)-1 : (T)1;
-        T v;
-        if constexpr (RULE == kRuleSp64) {
-            // the reference's P = prod_k t_k, then P / t_self (:231-241)
-            P = P * o[0];                     // every check has degree >= 1
+        P = P * o[0];                         // every check has degree >= 1
 #pragma unroll
-            for (int k = 1; k < DC; ++k) P = k < deg ? P * o[k] : P;
-            v = RuleMath<RULE>::two_atanh(P / tv);
-        } else {
-            // binary32 variant: the extrinsic product over the other edges in
-            // ascending order, no division. (P / t is 0/0 = NaN when b2c is
-            // exactly 0, which binary32 cancellation makes a ~1 % per-frame
-            // event at QBER 0.05, and the NaN then floods the frame.)
+        for (int k = 1; k < DC; ++k) P = k < deg ? P * o[k] : P;
+#ifdef QKD_EXP_NO_MATH
+        v = P + tv;
+#else
+        v = RuleMath<RULE>::two_atanh(P / tv);
+#endif
+    } else {
+        // binary32 variant: the extrinsic product over the other edges in
+        // ascending order, no division. (P / t is 0/0 = NaN when b2c is
+        // exactly 0, which binary32 cancellation makes a ~1 % per-frame
+        // event at QBER 0.05, and the NaN then floods the frame.)
+        T P = sbit ? (T)-1 : (T)1;
 #pragma unroll
-            for (int k = 0; k < DC; ++k) P = (k < deg && start + k != lane) ? P * o[k] : P;
-            v = RuleMath<RULE>::two_atanh(P);
-        }
-        if (CLAMP) v = clamp_msg(v, thr);
-        return v;
+        for (int k = 0; k < DC; ++k) P = (k < deg && start + k != lane) ? P * o[k] : P;
+        v = RuleMath<RULE>::two_atanh(P);
     }
+    if (CLAMP) v = clamp_msg(v, thr);
+    return v;
 }
 
-// The check phase of one iteration for one wave: tasks wave, wave+NW, ...
+// The check phase of one iteration for one wave: tasks wave, wave + NW, ...
+// Per edge (qkd_ldpc_algorithm.cpp:220-249):
+//   b2c = FIRST ? LLR_i : clamp(total_i - c2b)                  (:188, :303-316)
+//   t   = tanh(b2c / 2)                                         (:224)
+//   P   = (s_j ? -1 : 1) * t_0 * t_1 * ...  (ascending bits)    (:231-235)
+//   c2b = clamp(2 * atanh(P / t))                               (:239-249)
 // Software-pipelined and unrolled by two so that no loaded value is copied
 // across the loop back-edge. Each half-trip does, in this order:
 //   store the previous task's message  |  issue the look-ahead loads (plan
@@ -294,6 +314,12 @@ __device__ __forceinline__ T check_edge(T x, T old, uint32_t w, uint32_t sbit, i
 // for memory operations that had a whole task of arithmetic to complete.
 // The plan is padded with idle tasks (qkd_plan.h): no bounds tests on the
 // look-ahead loads.
+//
+// Measured (config 2, three iterations): removing the tanh /
+// atanh arithmetic saves only 12 % of the kernel, making the message
+// gathers/scatters coalesced saves 24 %: the phase is bound by the two
+// together, not by fp64 latency (working on two tasks at once, to interleave
+// two dependency chains, measured no gain).
 template <int SRC, bool CLAMP, int DC, int RULE, typename T>
 __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
                                             const T* total, const uint16_t* t2idx, const double* tab2,
@@ -304,7 +330,11 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
     int t = wave;
     if (t >= n_tasks) return;
     const uint2* pl = plan + lane;
+#ifdef QKD_EXP_MSG_LOCAL
+    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + lane + 64 * (wave & 7); };
+#else
     auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + pw_bit(p.x); };
+#endif
     // the incoming value: a bit total, or (kSrcTable) the tabulated tanh
     auto src = [&](uint2 p) -> T {
         if constexpr (SRC == kSrcTable) return tab2[t2idx[pw_bit(p.x)] + pw_row(p.x)];
@@ -312,6 +342,12 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
     };
     // the target syndrome bit of the lane's check
     auto sbit = [&](uint2 p) -> uint32_t { return (tsyn[p.y >> 5] >> (p.y & 31)) & 1u; };
+    auto edge = [&](T x, T o, uint2 w) -> T {
+        const T a = edge_in<SRC, CLAMP, RULE>(x, o, thr);
+        row[lane] = a;
+        wave_lds_sync();
+        return edge_out<CLAMP, DC, RULE>(a, w.x, sbit(w), lane, thr, row, ms_scale);
+    };
     uint2 wa = pl[t * 64];
     uint2 wb = pl[(t + NW) * 64];
     T xa = src(wa);
@@ -323,7 +359,7 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
         const uint2 wc = pl[(t + 2 * NW) * 64];
         const T xb = src(wb);
         const T ob = FIRST ? (T)0 : *msg(wb);
-        pv = check_edge<SRC, CLAMP, DC, RULE>(xa, oa, wa.x, sbit(wa), lane, thr, row, ms_scale);
+        pv = edge(xa, oa, wa);
         pend = msg(wa);
         t += NW;
         if (t >= n_tasks) break;
@@ -331,7 +367,7 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
         wa = pl[(t + 2 * NW) * 64];
         xa = src(wc);
         oa = FIRST ? (T)0 : *msg(wc);
-        pv = check_edge<SRC, CLAMP, DC, RULE>(xb, ob, wb.x, sbit(wb), lane, thr, row, ms_scale);
+        pv = edge(xb, ob, wb);
         pend = msg(wb);
         t += NW;
         if (t >= n_tasks) break;
@@ -469,7 +505,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     uint16_t* t2idx = reinterpret_cast<uint16_t*>(smem + L.t2idx);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    // wave index as a scalar: task loops and plan addresses stay in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     T* row = reinterpret_cast<T*>(smem + L.tval) + wave * (64 + DC);
     const int n_tasks = c.n_tasks;
     const int n_pad = c.n_pad;
@@ -521,7 +558,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                 }
                 total[i] = l;
             }
-            if (tid == 0) total[c.n] = 0;
+            if (tid == 0) {
+                total[c.n] = 0;
+                if (TABLES && a.tab2_entries) t2idx[c.n] = 0;   // idle lanes' table reads
+            }
         }
         // ---- prologue: target syndrome bits per check (tsyn) and, on the QKD
         //      path, each check's first-product sign (qsyn, fold_first_message);
@@ -678,10 +718,12 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             }
             const bool any_mismatch = block_any(mismatch, ctl + 2, any_k);
             pc.mark(3);
+#ifndef QKD_EXP_NO_STOP
             if (!any_mismatch) {
                 done = true;
                 break;
             }
+#endif
         }
 
         // ---- outputs: SP_result + last hard decision (+ keys_match)
