@@ -33,7 +33,8 @@ N_BITS = 10240
 # (4 E w) plus the LLR read (N w); per frame: Bob's bits in, decoded bits out,
 # syndrome in (2N + M bytes).
 E_EDGES, M_CHECKS, W = 30720, 5231, 8
-B_ITER = 4 * E_EDGES * W + N_BITS * W          # 1,064,960
+B_ITER = 4 * E_EDGES * W + N_BITS * W          # 1,064,960 (binary64 messages)
+B_ITER32 = 4 * E_EDGES * 4 + N_BITS * 4        # 532,480 (binary32 variants)
 B_FRAME = 2 * N_BITS + M_CHECKS                 # 25,711
 HBM_PEAK_GBS = 8000.0                           # MI355X_MICROARCH.md, HBM3E spec
 
@@ -52,6 +53,10 @@ def parse():
                     help="frames in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", default="sp_f64", choices=["sp_f64", "sp_f32", "minsum"],
+                    help="decoder rule of the headline line (sp_f64 = the reference's)")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the side measurement of the binary32 variants")
     return ap.parse_args()
 
 
@@ -71,6 +76,32 @@ def pmc_traffic():
     with open(files[-1]) as f:
         d = json.load(f)
     return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
+def measure_variants(args, step, stream, counters, iters, Q, F, q, steps=5):
+    """Side measurement on the same resident keys: the build-defined binary32
+    variants (QKD_VARIANT_SP_F32, QKD_VARIANT_MINSUM),
+    timed like the headline (wall clock over `steps` steps, HIP events for the
+    decode kernel). Their FER is a property of the decoder, not a parity claim."""
+    import torch
+    out = {}
+    for v in ("sp_f64", "sp_f32", "minsum"):
+        if v == args.variant:
+            continue
+        step(variant=v)
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(steps)]
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(evs[k], variant=v)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        st = Q.counters_to_stats(Q.read_counters(counters), F, args.max_iters, q)
+        out[v] = {"value": F * N_BITS * steps / el, "unit": "bit/s",
+                  "kernel_ms": float(np.mean([a.elapsed_time(b) for a, b in evs])),
+                  "fer": st["fer"], "mean_iterations": st["iterations_successful_sp_mean"]}
+    return out
 
 
 def cpu_baseline(args, g):
@@ -129,11 +160,12 @@ def main():
     L = Q._native.lib()
     sptr = int(stream.cuda_stream)
 
-    def step(ev=None):
+    def step(ev=None, variant=args.variant):
+        flags = Q.decoder_flags(True, variant)
         if ev is not None:
             ev[0].record(stream)
         Q._native.check(L.qkd_qkd_ldpc_batch(H.handle, ws.handle, alice.data_ptr(), bob.data_ptr(), F,
-                                             q, args.max_iters, args.threshold, Q.FLAG_THRESHOLD,
+                                             q, args.max_iters, args.threshold, flags,
                                              None, iters.data_ptr(), sp.data_ptr(), ko.data_ptr(), sptr))
         if ev is not None:
             ev[1].record(stream)
@@ -169,7 +201,8 @@ def main():
     value = frames_total * N_BITS * args.steps / elapsed
     # per-launch algorithmic bytes on this rank (executed iterations)
     sum_it_local = int(it_np.astype(np.int64).sum())
-    alg_bytes = sum_it_local * B_ITER + F * B_FRAME
+    b_iter = B_ITER if args.variant == "sp_f64" else B_ITER32
+    alg_bytes = sum_it_local * b_iter + F * B_FRAME
     avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9
     traffic, traffic_src = pmc_traffic()
@@ -187,7 +220,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64" if args.variant == "sp_f64" else "f32",
             "data": "synthetic: reference keygen (xoshiro256++ seed 777, exact-QBER error "
                     "injection) on the device; reference alist code N=10240",
             "config": {
@@ -195,6 +228,7 @@ def main():
                             f"QBER {args.qber}, <= {args.max_iters} iterations, clamp "
                             f"{args.threshold}, {F}-frame batch per GPU",
                 "frames_per_gpu": F,
+                "decoder": args.variant,
                 "parallelism": f"frames sharded over {world} GPU(s), counters all-reduced",
             },
             "fer": stats["fer"],
@@ -219,6 +253,8 @@ def main():
             names = ["prologue", "check", "bit", "syndrome", "fetch_out", "check_first", "check_second"]
             tot = float(cyc.sum()) or 1.0
             out["phase_share"] = {n: float(v) / tot for n, v in zip(names, cyc)}
+        if world == 1 and not args.no_variants:
+            out["variants"] = measure_variants(args, step, stream, counters, iters, Q, F, q)
         if world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
             out["cpu_baseline"] = cpu_baseline(args, g)
         print(json.dumps(out), flush=True)

@@ -36,10 +36,12 @@
 #include "qkd_rng.h"
 
 // Diagnostic builds only (tools/exp_run.sh; never the shipped library): the
-// QKD_EXP_NO_STOP / QKD_EXP_NO_MATH / QKD_EXP_MSG_LOCAL macros run a fixed
-// iteration count / drop the tanh-atanh arithmetic / make the check phase's
-// message accesses coalesced, to split the kernel's time between arithmetic
-// and memory. Results of such builds are wrong by design.
+// QKD_EXP_NO_STOP / QKD_EXP_NO_MATH / QKD_EXP_MSG_LOCAL / QKD_EXP_MSG_SMALL
+// macros run a fixed iteration count / drop the tanh-atanh arithmetic / make
+// the check phase's message accesses coalesced / keep them scattered but
+// within 4 KB per row (cache-resident), to split the kernel's time between
+// arithmetic, access pattern and footprint. Results of such
+// builds are wrong by design.
 
 namespace qkd {
 
@@ -58,7 +60,10 @@ enum DecodeMode : int {
 //               tanhf/atanhf (a variant: not bit-exact to anything)
 //   kRuleMinSum normalised min-sum in binary32: c2b = scale * sign * min|b2c|
 //               over the other edges of the check (a variant, no transcendental)
-enum DecodeRule : int { kRuleSp64 = 0, kRuleSp32 = 1, kRuleMinSum = 2 };
+//   kRuleMinSumLds  the same min-sum with the frame's whole message state in
+//               LDS (per check: min1, min2, argmin, sign bits), no global
+//               message store; used when the state fits (decode_ms_fits)
+enum DecodeRule : int { kRuleSp64 = 0, kRuleSp32 = 1, kRuleMinSum = 2, kRuleMinSumLds = 3 };
 template <int RULE> struct RuleMsg { using T = float; };
 template <> struct RuleMsg<kRuleSp64> { using T = double; };
 
@@ -154,9 +159,11 @@ __host__ __device__ inline int decode_m_words(int m) { return ((m + 63) / 64) * 
 //   tab2   [tab2_entries]   second-iteration tanh table
 //   t2idx  [n_pad]          per-bit base index into tab2 (uint16)
 //   ctl    [4]              frame index, block_any flags
+//   cst    [m] (uint4)      kRuleMinSumLds: per-check min-sum state (ms_state)
 struct DecodeLds {
-    size_t tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, bytes;
-    __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries, int esz) {
+    size_t tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, cst, bytes;
+    __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries, int esz,
+                                  int cst_checks = 0) {
         const int m_words = decode_m_words(m);
         tsyn = ((size_t)n_pad * esz + 15) & ~(size_t)15;
         xsyn = tsyn + (size_t)m_words * 4;
@@ -170,7 +177,8 @@ struct DecodeLds {
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         t2idx = tab2 + (size_t)tab2_entries * 8;
         ctl = (t2idx + (tab2_entries ? (size_t)n_pad * 2 : 0) + 15) & ~(size_t)15;
-        bytes = ctl + 16;
+        cst = ctl + 16;
+        bytes = cst + (size_t)cst_checks * 16;
     }
 };
 
@@ -332,6 +340,8 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
     const uint2* pl = plan + lane;
 #ifdef QKD_EXP_MSG_LOCAL
     auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + lane + 64 * (wave & 7); };
+#elif defined(QKD_EXP_MSG_SMALL)
+    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + (pw_bit(p.x) & 511); };
 #else
     auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + pw_bit(p.x); };
 #endif
@@ -375,6 +385,91 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
         wa = wc;
     }
     *pend = pv;
+}
+
+// ---- min-sum with the message state in LDS (kRuleMinSumLds) -----------------
+// Every min-sum message of a check j is a function of four words (ms_state):
+//   x  min1 = min_k |b2c_k|                (binary32 bits)
+//   y  min2 = min over k != idx1 of |b2c_k|
+//   z  sign bits, bit k = (b2c_k < 0)
+//   w  idx1 (bits 0..7; 0xff: none) | par << 31,   par = s_j ^ parity(z)
+// The message to the edge at position k is scale * (k == idx1 ? min2 : min1),
+// negated when par ^ z_k, then clamped: the same binary32 operations, on the
+// same values, as edge_out's min-sum branch (and its test specification, tests/test_variants.py), so the
+// two kernels agree bit for bit. (min over the others of the |b2c| is min2 for
+// the argmin and min1 for everyone else, ties included; NaN magnitudes never
+// win a comparison, as fminf ignores them.) 16 bytes per check instead of 4
+// bytes per edge: the frame's whole message state (m * 16 B) and its bit
+// totals (n * 4 B) stay in LDS, and the decode touches no global memory but
+// the code's own (L2-resident) arrays.
+template <bool CLAMP>
+__device__ __forceinline__ float ms_msg(uint4 st, uint32_t pos, float scale, float thr) {
+    const float m = pos == (st.w & 0xffu) ? __uint_as_float(st.y) : __uint_as_float(st.x);
+    float v = scale * m;
+    const uint32_t neg = (st.w >> 31) ^ ((st.z >> pos) & 1u);
+    v = neg ? -v : v;
+    if (CLAMP) v = clamp_msg(v, thr);
+    return v;
+}
+
+// Check phase of kRuleMinSumLds for one wave: per lane (edge), b2c from the
+// bit total and the check's previous state; the segment's first lane then
+// folds the segment's b2c (through the wave's LDS row) into the new state.
+// Check phase of kRuleMinSumLds: one THREAD per check (rounds of 1024
+// checks). The min-sum check rule costs a handful of operations per edge, so
+// unlike the sum-product phase (one edge per lane, to spread the per-edge
+// transcendentals) a thread walks its check's row itself: bit totals from
+// LDS, the previous state from LDS, the row's bits from the code's ELL array
+// (coalesced across threads, L2-resident), the next round's row loaded ahead.
+//   b2c_k = FIRST ? total : clamp(total - message_k(previous state))
+//   state = (min |b2c|, second min, argmin, signs, s_j ^ parity)
+template <int SRC, bool CLAMP, int DC>
+__device__ __forceinline__ void ms_check_phase(const DeviceCode& c, const uint32_t* tsyn, const float* total,
+                                               uint4* cst, float thr, float scale) {
+    const int m = c.m;
+    int j = threadIdx.x;
+    if (j >= m) return;
+    int nb[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) nb[k] = k < c.max_dc ? c.chk_bits[k * c.m_pad + j] : -1;
+    for (;;) {
+        int bl[DC];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) bl[k] = nb[k];
+        const int jn = j + kDecodeBlock;
+        if (jn < m) {
+#pragma unroll
+            for (int k = 0; k < DC; ++k) nb[k] = k < c.max_dc ? c.chk_bits[k * c.m_pad + jn] : -1;
+        }
+        uint4 st = make_uint4(0, 0, 0, 0);
+        if (SRC == kSrcGeneral) st = cst[j];
+        float m1 = __builtin_inff(), m2 = __builtin_inff();
+        uint32_t idx = 0xffu, sg = 0;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (bl[k] >= 0) {
+                float x = total[bl[k]];
+                if (SRC == kSrcGeneral) {
+                    x = x - ms_msg<CLAMP>(st, (uint32_t)k, scale, thr);
+                    if (CLAMP) x = clamp_msg(x, thr);
+                }
+                const float a = fabsf(x);
+                sg |= (x < 0.0f ? 1u : 0u) << k;
+                if (a < m1) {
+                    m2 = m1;
+                    m1 = a;
+                    idx = (uint32_t)k;
+                } else if (a < m2) {
+                    m2 = a;
+                }
+            }
+        }
+        const uint32_t sbit = (tsyn[j >> 5] >> (j & 31)) & 1u;
+        const uint32_t par = sbit ^ ((uint32_t)__popc(sg) & 1u);
+        cst[j] = make_uint4(__float_as_uint(m1), __float_as_uint(m2), sg, idx | (par << 31));
+        j = jn;
+        if (j >= m) break;
+    }
 }
 
 // Second check phase of the QKD path. After the first iteration every message
@@ -487,9 +582,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     // the exact QKD-path shortcuts (first/second-iteration tables) exist for
     // the reference rule only
     constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
+    constexpr bool MSL = RULE == kRuleMinSumLds;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
-    const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries, (int)sizeof(T));
+    const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries, (int)sizeof(T), MSL ? c.m : 0);
+    uint4* cst = reinterpret_cast<uint4*>(smem + L.cst);
     const int m_words = decode_m_words(c.m);
     T* total = reinterpret_cast<T*>(smem);
     uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
@@ -619,6 +716,13 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         uint32_t it = 0;
         for (; it < a.max_it; ++it) {
             bool tabled = false;
+            if constexpr (MSL) {
+                tabled = true;
+                if (it == 0)
+                    ms_check_phase<kSrcFirst, CLAMP, DC>(c, tsyn, total, cst, thr, a.ms_scale);
+                else
+                    ms_check_phase<kSrcGeneral, CLAMP, DC>(c, tsyn, total, cst, thr, a.ms_scale);
+            }
             if constexpr (TABLES) {
                 tabled = true;
                 if (it == 0 && fold1)
@@ -631,13 +735,15 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                 else
                     tabled = false;
             }
-            if (!tabled) {
-                if (it == 0)
-                    check_phase<kSrcFirst, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks,
-                                                            n_pad, thr, wave, lane, a.ms_scale);
-                else
-                    check_phase<kSrcGeneral, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks,
-                                                              n_pad, thr, wave, lane, a.ms_scale);
+            if constexpr (!MSL) {
+                if (!tabled) {
+                    if (it == 0)
+                        check_phase<kSrcFirst, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks,
+                                                                n_pad, thr, wave, lane, a.ms_scale);
+                    else
+                        check_phase<kSrcGeneral, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row,
+                                                                  n_tasks, n_pad, thr, wave, lane, a.ms_scale);
+                }
             }
             __syncthreads();
             pc.mark((TABLES && it < 2 && a.first_table) ? 5 + (int)it : 1);
@@ -648,6 +754,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kBitChunk) {
                 T v[kBitChunk][kDvUnroll];
                 int32_t jc[kBitChunk][kDvUnroll];
+                uint32_t ps[kBitChunk][kDvUnroll];     // MSL: positions in the checks
                 int dg[kBitChunk];
 #pragma unroll
                 for (int u = 0; u < kBitChunk; ++u) {
@@ -657,7 +764,12 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k) {
                         const bool ld = ok && k < c.max_dv;
-                        v[u][k] = (ld && !(fold1 && it == 0)) ? c2b[k * n_pad + i] : (T)0;
+                        if constexpr (MSL) {
+                            v[u][k] = 0;
+                            ps[u][k] = ld ? c.bit_pos[k * n_pad + i] : 0u;
+                        } else {
+                            v[u][k] = (ld && !(fold1 && it == 0)) ? c2b[k * n_pad + i] : (T)0;
+                        }
                         jc[u][k] = ld ? c.bit_chk[k * n_pad + i] : 0;
                     }
                 }
@@ -685,9 +797,20 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                             }
                         }
                     }
+                    if constexpr (MSL) {
+#pragma unroll
+                        for (int k = 0; k < kDvUnroll; ++k)
+                            if (k < deg) v[u][k] = ms_msg<CLAMP>(cst[jc[u][k]], ps[u][k], a.ms_scale, thr);
+                    }
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
-                    for (int k = kDvUnroll; k < deg; ++k) acc = acc + c2b[k * n_pad + i];
+                    if constexpr (MSL) {
+                        for (int k = kDvUnroll; k < deg; ++k)
+                            acc = acc + ms_msg<CLAMP>(cst[c.bit_chk[k * n_pad + i]], c.bit_pos[k * n_pad + i],
+                                                      a.ms_scale, thr);
+                    } else {
+                        for (int k = kDvUnroll; k < deg; ++k) acc = acc + c2b[k * n_pad + i];
+                    }
                     total[i] = acc;
                     if constexpr (TABLES) if (a.tab2_entries && it == 0) {
                         // second_table_index: bob bit and the signs of the first messages
@@ -1015,8 +1138,13 @@ static DecodeFn pick_decode_dc(int max_dc, int* dc) {
     if (max_dc <= 6) { *dc = 6; return decode_kernel<MODE, RULE, 6, CLAMP>; }
     if (max_dc <= 8) { *dc = 8; return decode_kernel<MODE, RULE, 8, CLAMP>; }
     if (max_dc <= 16) { *dc = 16; return decode_kernel<MODE, RULE, 16, CLAMP>; }
-    *dc = 64;
-    return decode_kernel<MODE, RULE, 64, CLAMP>;
+    if constexpr (RULE == kRuleMinSumLds) {       // decode_ms_fits: degree <= 32
+        *dc = 32;
+        return decode_kernel<MODE, RULE, 32, CLAMP>;
+    } else {
+        *dc = 64;
+        return decode_kernel<MODE, RULE, 64, CLAMP>;
+    }
 }
 
 template <int MODE, int RULE>
@@ -1028,6 +1156,7 @@ template <int MODE>
 static DecodeFn pick_decode_rule(int rule, bool clamp, int max_dc, int* dc) {
     if (rule == kRuleSp32) return pick_decode_clamp<MODE, kRuleSp32>(clamp, max_dc, dc);
     if (rule == kRuleMinSum) return pick_decode_clamp<MODE, kRuleMinSum>(clamp, max_dc, dc);
+    if (rule == kRuleMinSumLds) return pick_decode_clamp<MODE, kRuleMinSumLds>(clamp, max_dc, dc);
     return pick_decode_clamp<MODE, kRuleSp64>(clamp, max_dc, dc);
 }
 
@@ -1050,7 +1179,17 @@ static float minsum_scale_of(uint32_t flags) {
 }
 
 static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries, int rule) {
-    return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries, rule == kRuleSp64 ? 8 : 4).bytes;
+    return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries, rule == kRuleSp64 ? 8 : 4,
+                     rule == kRuleMinSumLds ? c->m : 0).bytes;
+}
+
+// The LDS-resident min-sum needs the check state (sign bits in one word:
+// degree <= 32) and all of its LDS in one workgroup.
+static constexpr size_t kLdsBytesMax = 160 * 1024;
+static bool decode_ms_fits(const qkd_code* c) {
+    if (c->max_dc > 32) return false;
+    const int dc = c->max_dc <= 4 ? 4 : c->max_dc <= 6 ? 6 : c->max_dc <= 8 ? 8 : c->max_dc <= 16 ? 16 : 32;
+    return decode_lds_bytes(c, dc, 0, kRuleMinSumLds) <= kLdsBytesMax;
 }
 
 // Resident workgroups of decode_kernel for this code on its device.
@@ -1144,7 +1283,11 @@ static unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 
 static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs& a, int mode,
                                 uint32_t flags, hipStream_t stream) {
     int dc = 0;
-    const int rule = rule_of(flags);
+    int rule = rule_of(flags);
+    // QKD_MINSUM_STORE=global keeps the global-message-store min-sum (tests)
+    const char* ms_store = getenv("QKD_MINSUM_STORE");
+    const bool ms_global = ms_store && !strcmp(ms_store, "global");
+    if (rule == kRuleMinSum && !ms_global && decode_ms_fits(c)) rule = kRuleMinSumLds;
     a.ms_scale = minsum_scale_of(flags);
     DecodeFn fn = pick_decode(mode, rule, a.clamp_on != 0, c->max_dc, &dc);
     const size_t lds = decode_lds_bytes(c, dc, a.tab2_entries, rule);
@@ -1152,7 +1295,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     qkd_status s = decode_grid(c, fn, lds, &grid);
     if (s != QKD_OK) return s;
     grid = (int)std::min<size_t>((size_t)grid, a.n_frames);
-    s = ws_reserve_decode(ws, (size_t)grid);
+    s = ws_reserve_decode(ws, rule == kRuleMinSumLds ? 0 : (size_t)grid);   // no global messages
     if (s != QKD_OK) return s;
     a.code = c->view();
     a.c2b = ws->c2b;

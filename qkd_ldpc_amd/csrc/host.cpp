@@ -39,8 +39,8 @@ static void free_device(qkd_code* c) {
     if (c->d_chk_bits) (void)hipFree(c->d_chk_bits);
     if (c->d_chk_deg) (void)hipFree(c->d_chk_deg);
     if (c->d_bit_chk) (void)hipFree(c->d_bit_chk);
-    if (c->d_bit_slot) (void)hipFree(c->d_bit_slot);
-    c->d_bit_slot = nullptr;
+    if (c->d_bit_pos) (void)hipFree(c->d_bit_pos);
+    c->d_bit_pos = nullptr;
     if (c->d_bit_deg) (void)hipFree(c->d_bit_deg);
     if (c->d_bit_pat) (void)hipFree(c->d_bit_pat);
     if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
@@ -114,6 +114,7 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     std::vector<int32_t> chk_bits((size_t)max_dc * c->m_pad, -1);
     std::vector<uint8_t> chk_deg(m, 0);
     std::vector<int32_t> bit_chk((size_t)max_dv * c->n_pad, -1);
+    std::vector<uint8_t> bit_pos((size_t)max_dv * c->n_pad, 0);
     std::vector<uint8_t> bit_deg(n, 0);
     std::vector<int32_t> krow(e, 0);
     for (int32_t j = 0; j < m; ++j) {
@@ -125,6 +126,7 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
             const int32_t bk = fill[b] - c->bit_ptr[b];
             c->bit_idx[fill[b]++] = j;
             bit_chk[(size_t)bk * c->n_pad + b] = j;
+            bit_pos[(size_t)bk * c->n_pad + b] = (uint8_t)slot;
             krow[k] = bk;
         }
     }
@@ -132,16 +134,6 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     if (!qkdp::build_wave_plan(n, m, cptr, cidx, krow.data(), plan))
         return set_error(QKD_ERR_UNSUPPORTED, "check degree outside [1, %d]", qkdp::kPlanMaxDegree);
     c->n_tasks = plan.n_tasks;
-    std::vector<int32_t> bit_slot((size_t)max_dv * c->n_pad, 0);
-    {
-        std::vector<int32_t> fill2(c->bit_ptr.begin(), c->bit_ptr.end() - 1);
-        for (int32_t j = 0; j < m; ++j)
-            for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) {
-                const int32_t b = cidx[k];
-                const int32_t bk = fill2[b]++ - c->bit_ptr[b];
-                bit_slot[(size_t)bk * c->n_pad + b] = plan.slot_of_edge[k];
-            }
-    }
     // degree patterns of the bits: the ascending checks' degrees
     std::vector<uint16_t> bit_pat(n, 0);
     c->n_pat = 0;
@@ -189,8 +181,8 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     QKD_HIP(hipMemcpy(c->d_chk_bits, chk_bits.data(), chk_bits.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_chk_deg, chk_deg.data(), chk_deg.size(), hipMemcpyHostToDevice));
-    QKD_HIP(hipMalloc(&c->d_bit_slot, bit_slot.size() * sizeof(int32_t)));
-    QKD_HIP(hipMemcpy(c->d_bit_slot, bit_slot.data(), bit_slot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    QKD_HIP(hipMalloc(&c->d_bit_pos, bit_pos.size()));
+    QKD_HIP(hipMemcpy(c->d_bit_pos, bit_pos.data(), bit_pos.size(), hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_bit_chk, bit_chk.data(), bit_chk.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_bit_deg, bit_deg.data(), bit_deg.size(), hipMemcpyHostToDevice));

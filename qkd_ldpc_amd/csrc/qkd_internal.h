@@ -38,8 +38,8 @@ constexpr uint32_t kKeygenFastMaxErrors = 4096;
 //                            s = task*64 + lane holds one edge: {plan word,
 //                            check index}
 //   bit_chk[k * n_pad + i]   k-th check of bit i (ascending), -1 pad
-//   bit_slot[k * n_pad + i]  plan slot of that edge (c2b messages are stored
-//                            per frame in plan order)
+//   bit_pos[k * n_pad + i]   position of bit i in that check's ascending row
+//                            (LDS min-sum state lookups)
 // Slot-major ("ELL") layouts keep lane-consecutive bits on consecutive
 // addresses.
 struct DeviceCode {
@@ -51,7 +51,7 @@ struct DeviceCode {
     const uint8_t* chk_deg;
     const uint2* plan;            // {plan word, check index (0 on idle lanes)}
     const int32_t* bit_chk;
-    const int32_t* bit_slot;
+    const uint8_t* bit_pos;
     const uint8_t* bit_deg;
     // degree patterns of the bits (second-iteration tanh table, decode.hip):
     // bit_pat[i] = pattern of bit i; pat_deg[p * max_dv + k] = degree of the
@@ -92,7 +92,7 @@ struct qkd_code {
     int32_t* d_chk_bits = nullptr;
     uint8_t* d_chk_deg = nullptr;
     int32_t* d_bit_chk = nullptr;
-    int32_t* d_bit_slot = nullptr;
+    uint8_t* d_bit_pos = nullptr;
     uint8_t* d_bit_deg = nullptr;
     uint2* d_plan = nullptr;
     int32_t n_pat = 0;                  // 0: too many degree patterns for the table
@@ -108,7 +108,7 @@ struct qkd_code {
 
     qkd::DeviceCode view() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, n_tasks,
-                               d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_slot, d_bit_deg,
+                               d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
                                n_pat, d_bit_pat, d_pat_deg};
     }
 };

@@ -38,7 +38,7 @@ namespace qkdp {
 
 constexpr uint32_t kPlanBitMask = 0x7FFFu;
 constexpr int kPlanMaxBits = (int)kPlanBitMask;    // N must be < this (dummy column N)
-constexpr int kPlanPadTasks = 64;                  // idle tasks appended to the plan
+constexpr int kPlanPadTasks = 128;                 // idle tasks appended to the plan
 constexpr int kPlanMaxDegree = 64;                 // check degree: one wavefront
 constexpr int kPlanMaxBitDegree = 32;              // bit degree: 5-bit row index
 

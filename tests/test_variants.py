@@ -97,7 +97,13 @@ def _dev(x, dtype):
     (0.05, 50, 0.0, False, None),
     (0.10, 3, 0.7, True, 255 / 256),
 ])
-def test_minsum_llr_bit_exact(Q, H, ms_model, oracle_mod, q, max_it, thr, thr_on, scale):
+@pytest.mark.parametrize("store", ["lds", "global"])
+def test_minsum_llr_bit_exact(Q, H, ms_model, oracle_mod, monkeypatch, store, q, max_it, thr, thr_on,
+                              scale):
+    """Both min-sum kernels: the frame state in LDS (per-check min1/min2/argmin/
+    signs, the default where it fits) and the per-edge global message store."""
+    if store == "global":
+        monkeypatch.setenv("QKD_MINSUM_STORE", "global")
     A, B, qq = _frames(oracle_mod, q, 48, seed=int(q * 1000) + max_it)
     lp = np.log((1 - qq) / qq)
     llr = np.where(B == 1, -lp, lp)
@@ -130,7 +136,10 @@ def test_minsum_keys_path_bit_exact(Q, H, ms_model, oracle_mod):
 
 
 @pytest.mark.gpu
-def test_minsum_small_codes_bit_exact(Q, dense_codes):
+@pytest.mark.parametrize("store", ["lds", "global"])
+def test_minsum_small_codes_bit_exact(Q, dense_codes, monkeypatch, store):
+    if store == "global":
+        monkeypatch.setenv("QKD_MINSUM_STORE", "global")
     rng = np.random.default_rng(17)
     for name, dense in dense_codes.items():
         m, n = dense.shape
