@@ -395,7 +395,7 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
 //   w  idx1 (bits 0..7; 0xff: none) | par << 31,   par = s_j ^ parity(z)
 // The message to the edge at position k is scale * (k == idx1 ? min2 : min1),
 // negated when par ^ z_k, then clamped: the same binary32 operations, on the
-// same values, as edge_out's min-sum branch (and its test specification, tests/test_variants.py), so the
+// same values, as edge_out's min-sum branch (and tests/test_variants.py's model), so the
 // two kernels agree bit for bit. (min over the others of the |b2c| is min2 for
 // the argmin and min1 for everyone else, ties included; NaN magnitudes never
 // win a comparison, as fminf ignores them.) 16 bytes per check instead of 4
