@@ -36,6 +36,7 @@
 #include "../include/qkd_ldpc.h"
 #include "qkd_amd_extensions.hpp"
 #include "qkd_reference_api.hpp"
+#include "qkd_sim_stats.hpp"
 
 namespace {
 
@@ -352,25 +353,12 @@ std::vector<sim_result> QKD_LDPC_batch_simulation(const std::vector<sim_input>& 
         for (double QBER : in.QBER) {
             const std::vector<trial_result> tr =
                 qkd_amd_run_trials(matrix, QBER, seeds.data(), seeds.size(), curr_sim);
-            size_t ok_sp = 0, ok_ldpc = 0, it_max = 0, it_min = CFG.SUM_PRODUCT_MAX_ITERATIONS;
-            double mean = 0, std_dev = 0;
-            for (const auto& r : tr) {
-                if (!r.ldpc_res.sp_res.syndromes_match) continue;
-                ok_sp++;
-                const size_t it = r.ldpc_res.sp_res.iterations_num;
-                it_max = std::max(it_max, it);
-                it_min = std::min(it_min, it);
-                if (r.ldpc_res.keys_match) ok_ldpc++;
-                mean += static_cast<double>(it);
-            }
-            if (ok_sp > 0) {
-                mean /= static_cast<double>(ok_sp);
-                for (const auto& r : tr)
-                    if (r.ldpc_res.sp_res.syndromes_match)
-                        std_dev += std::pow(static_cast<double>(r.ldpc_res.sp_res.iterations_num) - mean, 2);
-                std_dev /= static_cast<double>(ok_sp);
-                std_dev = std::sqrt(std_dev);
-            }
+            const qkdsim::PointStats st = qkdsim::reduce_point(
+                tr.size(), CFG.SUM_PRODUCT_MAX_ITERATIONS, [&](size_t k, bool& sp, bool& ko, size_t& it) {
+                    sp = tr[k].ldpc_res.sp_res.syndromes_match;
+                    ko = tr[k].ldpc_res.keys_match;
+                    it = tr[k].ldpc_res.sp_res.iterations_num;
+                });
             sim_result& s = out[curr_sim];
             s.sim_number = curr_sim;
             s.matrix_filename = matrix_filename;
@@ -378,12 +366,12 @@ std::vector<sim_result> QKD_LDPC_batch_simulation(const std::vector<sim_input>& 
             s.num_bit_nodes = matrix.num_bit_nodes;
             s.num_check_nodes = matrix.num_check_nodes;
             s.initial_QBER = tr.empty() ? 0.0 : tr[0].initial_QBER;
-            s.iterations_successful_sp_max = it_max;
-            s.iterations_successful_sp_min = (it_min == CFG.SUM_PRODUCT_MAX_ITERATIONS) ? 0 : it_min;
-            s.iterations_successful_sp_mean = mean;
-            s.iterations_successful_sp_std_dev = std_dev;
-            s.ratio_trials_successful_ldpc = static_cast<double>(ok_ldpc) / CFG.TRIALS_NUMBER;
-            s.ratio_trials_successful_sp = static_cast<double>(ok_sp) / CFG.TRIALS_NUMBER;
+            s.iterations_successful_sp_max = st.iterations_successful_sp_max;
+            s.iterations_successful_sp_min = st.iterations_successful_sp_min;
+            s.iterations_successful_sp_mean = st.iterations_successful_sp_mean;
+            s.iterations_successful_sp_std_dev = st.iterations_successful_sp_std_dev;
+            s.ratio_trials_successful_ldpc = st.ratio_trials_successful_ldpc;
+            s.ratio_trials_successful_sp = st.ratio_trials_successful_sp;
             curr_sim++;
         }
     }
