@@ -200,6 +200,20 @@ QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t 
  * reference counterpart (the reference prints TRACE_* arrays instead,
  * qkd_ldpc_algorithm.cpp:42-155). */
 QKD_API qkd_status qkd_debug_phase_cycles(qkd_workspace *ws, uint64_t *cycles7);
+/* Trace of one frame, the reference's TRACE_SUM_PRODUCT / TRACE_SUM_PRODUCT_LLR
+ * (qkd_ldpc_algorithm.cpp:212-330): decodes llr[N] / syndrome[M] (host arrays)
+ * with the reference rule (QKD_VARIANT_SP_F64 only) and records, for every
+ * executed iteration t < *iterations, the messages the reference prints:
+ *   c2b_trace[t*E + e]   "E:" check-to-bit messages after the clamp, in the
+ *                        reference's check_to_bit_msg order (bit by bit, each
+ *                        bit's checks ascending; bit_ptr of get_adjacency)
+ *   total_trace[t*N + i] "L:" bit totals
+ * (host arrays of max_iterations*E / *N, either may be NULL). "z:", "s:",
+ * "M:" and MAX_LLR follow from these exactly (qkd_ldpc_amd.trace_decode). */
+QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, const uint8_t *syndrome,
+                                    uint32_t max_iterations, double msg_threshold, uint32_t flags,
+                                    double *c2b_trace, double *total_trace, uint32_t *iterations,
+                                    uint8_t *syndrome_match);
 /* The decoder's tanh (which = 0) / atanh (which = 1) restatement applied to
  * x[n] -> y[n] (device arrays): the bit-exactness check of the device build
  * against glibc (reference qkd_ldpc_algorithm.cpp:224, :241). which = 2 / 3:

@@ -354,7 +354,7 @@ static uint64_t fnv_doubles(const double *v, int cnt) {
 ORC_API int orc_decode(const orc_code *h, const double *llr, const int *syndrome,
                        int max_it, double thr, int thr_enable, int *out,
                        int *iters, int *sp_ok, uint64_t *fp, int *n_fp, double *ltrace,
-                       double *max_llr) {
+                       double *max_llr, double *etrace) {
     const int n = h->n, m = h->m, e = h->chk_off[m];
     double *b2c = (double *)malloc(sizeof(double) * (size_t)(e ? e : 1));
     double *c2b = (double *)malloc(sizeof(double) * (size_t)(h->bit_off[n] ? h->bit_off[n] : 1));
@@ -383,6 +383,8 @@ ORC_API int orc_decode(const orc_code *h, const double *llr, const int *syndrome
             }
         }
         if (thr_enable) clamp_msgs(c2b, h->bit_off[n], thr);                /* :246-249 */
+        if (etrace)                                /* TRACE_SUM_PRODUCT "E:", :250-254 */
+            memcpy(etrace + (size_t)it * h->bit_off[n], c2b, sizeof(double) * (size_t)h->bit_off[n]);
         if (fp) fp[nfp] = fnv_doubles(c2b, h->bit_off[n]);
         nfp++;
         for (int i = 0; i < n; i++) {                                      /* :256-267 */
@@ -433,7 +435,7 @@ ORC_API int orc_qkd_ldpc(const orc_code *h, const int *alice, const int *bob, do
     int *dec = out ? out : (int *)malloc(sizeof(int) * (size_t)n);
     for (int i = 0; i < n; i++) llr[i] = bob[i] ? -log_p : log_p;          /* :402-405 */
     orc_syndrome(h, alice, syn);                                           /* :413-414 */
-    orc_decode(h, llr, syn, max_it, thr, thr_enable, dec, iters, sp_ok, NULL, NULL, NULL, NULL);
+    orc_decode(h, llr, syn, max_it, thr, thr_enable, dec, iters, sp_ok, NULL, NULL, NULL, NULL, NULL);
     int eq = 1;
     for (int i = 0; i < n; i++) if (alice[i] != dec[i]) { eq = 0; break; } /* :433 */
     *key_ok = eq;

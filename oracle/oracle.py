@@ -52,7 +52,7 @@ def lib():
         L.orc_decode.restype = C.c_int
         L.orc_decode.argtypes = [P, f64p, i32p, C.c_int, C.c_double, C.c_int, i32p,
                                  C.POINTER(C.c_int), C.POINTER(C.c_int), P, C.POINTER(C.c_int), P,
-                                 C.POINTER(C.c_double)]
+                                 C.POINTER(C.c_double), P]
         L.orc_qkd_ldpc.argtypes = [P, i32p, i32p, C.c_double, C.c_int, C.c_double, C.c_int,
                                    C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), P]
         L.orc_run_trial.restype = C.c_int
@@ -122,21 +122,25 @@ class Code:
         return out
 
     def decode(self, llr, syndrome, max_it=50, thr=100.0, thr_enable=True,
-               fingerprints=False, ltrace=False):
+               fingerprints=False, ltrace=False, etrace=False):
         llr = np.ascontiguousarray(llr, dtype=np.float64)
         syn = np.ascontiguousarray(syndrome, dtype=np.int32)
         out = np.zeros(self.n, np.int32)
         it, ok, nfp, mx = C.c_int(), C.c_int(), C.c_int(), C.c_double()
         fp = np.zeros(2 * max_it, np.uint64) if fingerprints else None
         lt = np.zeros((max_it, self.n), np.float64) if ltrace else None
+        et = np.zeros((max_it, self.e), np.float64) if etrace else None
         lib().orc_decode(self.h, llr, syn, max_it, thr, int(thr_enable), out, C.byref(it),
                          C.byref(ok), fp.ctypes.data if fp is not None else None, C.byref(nfp),
-                         lt.ctypes.data if lt is not None else None, C.byref(mx))
+                         lt.ctypes.data if lt is not None else None, C.byref(mx),
+                         et.ctypes.data if et is not None else None)
         res = {"iters": it.value, "sp_ok": bool(ok.value), "out": out, "max_llr": mx.value}
         if fp is not None:
             res["fingerprints"] = [int(x) for x in fp[: nfp.value]]
         if lt is not None:
             res["ltrace"] = lt[: it.value]
+        if et is not None:
+            res["etrace"] = et[: it.value]     # c2b after the clamp, bit-major (bit_off order)
         return res
 
     def qkd_ldpc(self, alice, bob, q, max_it=50, thr=100.0, thr_enable=True):

@@ -38,7 +38,7 @@ __all__ = [
     "HMatrix", "QkdError", "calculate_syndrome", "sum_product_decoding",
     "sum_product_decoding_irregular", "sum_product_decoding_regular", "qkd_ldpc",
     "QKD_LDPC_irregular", "QKD_LDPC_regular", "keygen", "run_trials", "make_seeds",
-    "qber_range", "Workspace", "counters_to_stats", "decoder_flags",
+    "qber_range", "Workspace", "counters_to_stats", "decoder_flags", "trace_decode",
 ]
 
 
@@ -310,6 +310,65 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                                      _ptr(out.keys_match), _ptr(out.exact_qber),
                                      _ptr(out.counters), _stream(stream)))
     return out
+
+
+def trace_decode(H: HMatrix, llr, syndrome, max_iterations: int = 50, msg_threshold: float = 100.0,
+                 threshold_enabled: bool = True) -> dict:
+    """TRACE_SUM_PRODUCT / TRACE_SUM_PRODUCT_LLR of the reference decoder
+    (qkd_ldpc_algorithm.cpp:212-330) for one frame, decoded on the device.
+    llr [N] float64 and syndrome [M] 0/1 as host arrays. Returns per executed
+    iteration t the arrays the reference prints:
+      E[t]  check-to-bit messages after the clamp, bit by bit (each bit's checks
+            ascending) - the reference's check_to_bit_msg rows
+      L[t]  bit totals;  z[t] hard decision;  s[t] its syndrome
+      M[t]  bit-to-check messages after the clamp, check by check (each check's
+            bits ascending) - bit_to_check_msg; only for iterations that did not
+            stop (the reference computes M after the syndrome test)
+    and max_llr (MAX_LLR: the largest |E|, |M| over those iterations)."""
+    llr = np.ascontiguousarray(llr, dtype=np.float64)
+    syn = np.ascontiguousarray(np.asarray(syndrome) != 0, dtype=np.uint8)
+    n, m = H.num_bit_nodes, H.num_check_nodes
+    cptr, cidx, bptr, bidx = H.adjacency()
+    e = len(cidx)
+    E = np.zeros((max_iterations, e), np.float64)
+    L = np.zeros((max_iterations, n), np.float64)
+    it = C.c_uint32()
+    ok = C.c_uint8()
+    flags = decoder_flags(threshold_enabled, "sp_f64")
+    N.check(N.lib().qkd_trace_decode(H.handle, llr.ctypes.data, syn.ctypes.data, max_iterations,
+                                     msg_threshold, flags, E.ctypes.data, L.ctypes.data,
+                                     C.byref(it), C.byref(ok)))
+    t_n = it.value
+    E, L = E[:t_n], L[:t_n]
+    z = (L <= 0).astype(np.uint8)
+    # s: calculate_syndrome of each hard decision
+    chk_of = np.repeat(np.arange(m), np.diff(cptr))
+    s = np.zeros((t_n, m), np.uint8)
+    for t in range(t_n):
+        np.bitwise_xor.at(s[t], chk_of, z[t][cidx])
+    # M: b2c[j][pos] = clamp(L_i - E[i][k]) for the edge (bit i's k-th check j)
+    bit_of_e = np.repeat(np.arange(n), np.diff(bptr))
+    pos_in_check = {}
+    for j in range(m):
+        for p, b in enumerate(cidx[cptr[j]:cptr[j + 1]]):
+            pos_in_check[(j, int(b))] = cptr[j] + p
+    to_check_order = np.array([pos_in_check[(int(bidx[k]), int(bit_of_e[k]))] for k in range(e)])
+    stopped = bool(ok.value)
+    t_m = t_n - 1 if stopped else t_n
+    M = np.zeros((t_m, e), np.float64)
+    max_llr = 0.0
+    for t in range(t_m):
+        b2c = L[t][bit_of_e] - E[t]
+        if threshold_enabled:
+            b2c = np.where(b2c > msg_threshold, msg_threshold, np.where(b2c < -msg_threshold, -msg_threshold, b2c))
+        M[t][to_check_order] = b2c
+        for arr in (E[t], M[t]):
+            a = np.abs(arr)
+            a = a[~np.isnan(a)]
+            if a.size:
+                max_llr = max(max_llr, float(a.max()))
+    return {"iterations": t_n, "syndromes_match": stopped, "E": E, "L": L, "z": z, "s": s, "M": M,
+            "max_llr": max_llr}
 
 
 def read_counters(counters) -> N.Counters:

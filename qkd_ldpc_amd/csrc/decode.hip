@@ -103,6 +103,10 @@ struct DecodeArgs {
     // diagnostics: per-phase shader-clock cycles summed over workgroups
     // (thread 0's view between barriers), or nullptr
     unsigned long long* phase;
+    // qkd_trace_decode (binary64 rule, one frame): per executed iteration, the
+    // c2b store (max_dv x n_pad) then the bit totals (n_pad), or nullptr
+    double* trace;
+    size_t trace_stride;
 };
 
 // Phase-clock accumulation (diagnostic; a wave-uniform test when off). Each
@@ -833,6 +837,15 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             }
             __syncthreads();
             pc.mark(2);
+            if constexpr (RULE == kRuleSp64) {
+                // TRACE_SUM_PRODUCT (:250-275): this iteration's clamped c2b ("E") and totals ("L")
+                if (a.trace) {
+                    double* tr = a.trace + (size_t)it * a.trace_stride;
+                    const int nm = c.max_dv * n_pad;
+                    for (int q = tid; q < nm; q += kDecodeBlock) tr[q] = c2b[q];
+                    for (int q = tid; q < c.n; q += kDecodeBlock) tr[nm + q] = total[q];
+                }
+            }
             // syndrome test (:285): any word differing from the target
             bool mismatch = false;
             for (int w = tid; w < m_words; w += kDecodeBlock) {
@@ -1536,6 +1549,82 @@ qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void*
                        x, y, n);
     QKD_HIP(hipGetLastError());
     return QKD_OK;
+}
+
+qkd_status qkd_trace_decode(const qkd_code* c, const double* llr, const uint8_t* syndrome,
+                            uint32_t max_iterations, double msg_threshold, uint32_t flags,
+                            double* c2b_trace, double* total_trace, uint32_t* iterations,
+                            uint8_t* syndrome_match) {
+    clear_error();
+    if (!c || !llr || !syndrome || !iterations || !syndrome_match)
+        return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    qkd_status s = check_decode_params(max_iterations, msg_threshold, flags);
+    if (s != QKD_OK) return s;
+    if ((flags & QKD_VARIANT_MASK) != QKD_VARIANT_SP_F64)
+        return set_error(QKD_ERR_UNSUPPORTED, "trace is provided for the reference rule (QKD_VARIANT_SP_F64) only");
+    DeviceGuard g(c->device);
+    qkd_workspace* ws = qkd_workspace_create(c, &s);
+    if (!ws) return s;
+    const size_t stride = (size_t)c->max_dv * c->n_pad + c->n_pad;
+    double *d_llr = nullptr, *d_tr = nullptr;
+    uint8_t *d_syn = nullptr, *d_ok = nullptr;
+    uint32_t* d_it = nullptr;
+    auto cleanup = [&]() {
+        for (void* p : {(void*)d_llr, (void*)d_tr, (void*)d_syn, (void*)d_ok, (void*)d_it})
+            if (p) (void)hipFree(p);
+        qkd_workspace_destroy(ws);
+    };
+    hipStream_t st = nullptr;
+    if (hipMalloc(&d_llr, (size_t)c->n * 8) != hipSuccess || hipMalloc(&d_syn, (size_t)c->m) != hipSuccess ||
+        hipMalloc(&d_ok, 1) != hipSuccess || hipMalloc(&d_it, 4) != hipSuccess ||
+        hipMalloc(&d_tr, stride * max_iterations * 8) != hipSuccess) {
+        cleanup();
+        return set_error(QKD_ERR_OUT_OF_MEMORY, "trace: cannot allocate %zu B", stride * max_iterations * 8);
+    }
+    std::vector<uint8_t> syn01((size_t)c->m);
+    for (int32_t j = 0; j < c->m; ++j) syn01[j] = syndrome[j] ? 1 : 0;
+    hipError_t e = hipMemcpy(d_llr, llr, (size_t)c->n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_syn, syn01.data(), (size_t)c->m, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        cleanup();
+        return set_error(QKD_ERR_DEVICE, "trace: %s", hipGetErrorString(e));
+    }
+    DecodeArgs a{};
+    a.n_frames = 1;
+    a.max_it = max_iterations;
+    a.thr = msg_threshold;
+    a.clamp_on = (flags & QKD_FLAG_THRESHOLD) ? 1 : 0;
+    a.llr = d_llr;
+    a.syn = d_syn;
+    a.iters = d_it;
+    a.sp_ok = d_ok;
+    a.trace = d_tr;
+    a.trace_stride = stride;
+    s = launch_decode(c, ws, a, kModeLlr, flags, st);
+    if (s == QKD_OK) {
+        std::vector<double> tr(stride * max_iterations);
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = hipMemcpy(iterations, d_it, 4, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(syndrome_match, d_ok, 1, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(tr.data(), d_tr, tr.size() * 8, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            s = set_error(QKD_ERR_DEVICE, "trace: %s", hipGetErrorString(e));
+        } else {
+            // bit-major jagged order of the reference's check_to_bit_msg rows
+            const size_t nm = (size_t)c->max_dv * c->n_pad;
+            for (uint32_t t = 0; t < *iterations; ++t) {
+                const double* src = tr.data() + t * stride;
+                if (c2b_trace)
+                    for (int32_t i = 0; i < c->n; ++i)
+                        for (int32_t k = 0; k < c->bit_ptr[i + 1] - c->bit_ptr[i]; ++k)
+                            c2b_trace[(size_t)t * c->e + c->bit_ptr[i] + k] = src[(size_t)k * c->n_pad + i];
+                if (total_trace)
+                    for (int32_t i = 0; i < c->n; ++i) total_trace[(size_t)t * c->n + i] = src[nm + i];
+            }
+        }
+    }
+    cleanup();
+    return s;
 }
 
 qkd_status qkd_debug_phase_cycles(qkd_workspace* ws, uint64_t* cycles7) {
