@@ -23,8 +23,10 @@
 //
 //   qkd_ldpc_sim [--root DIR] [--config FILE] [--matrix-dir DIR] [--results-dir DIR]
 //                [--gpus N | --devices i,j,...] [--variant sp_f64|sp_f32|minsum]
-//                [--dry-run] [--quiet]
+//                [--dry-run] [--sort-rows] [--quiet]
 //
+// --sort-rows reads alist files whose lines are not ascending (rejected by
+// default: the reference would mis-route their messages).
 // DIR defaults to the current directory and plays the reference's SOURCE_DIR:
 // DIR/config.json, DIR/dense_matrices, DIR/alist_sparse_matrices, DIR/results.
 #include <hip/hip_runtime_api.h>
@@ -264,7 +266,7 @@ struct Args {
     fs::path root = ".", config, matrix_dir, results_dir;
     std::vector<int> devices{0};
     uint32_t variant = QKD_VARIANT_SP_F64;
-    bool quiet = false, dry_run = false;
+    bool quiet = false, dry_run = false, sort_rows = false;
 };
 
 Args parse_args(int argc, char** argv) {
@@ -293,6 +295,7 @@ Args parse_args(int argc, char** argv) {
             if (a.devices.empty()) throw std::runtime_error("--devices needs at least one index");
         } else if (k == "--quiet") a.quiet = true;
         else if (k == "--dry-run") a.dry_run = true;
+        else if (k == "--sort-rows") a.sort_rows = true;
         else if (k == "--variant") {
             const std::string v = next();
             if (v == "sp_f64") a.variant = QKD_VARIANT_SP_F64;
@@ -302,7 +305,7 @@ Args parse_args(int argc, char** argv) {
         } else if (k == "-h" || k == "--help") {
             std::printf("usage: qkd_ldpc_sim [--root DIR] [--config FILE] [--matrix-dir DIR] [--results-dir DIR]\n"
                         "                    [--gpus N | --devices i,j,...] [--variant sp_f64|sp_f32|minsum]\n"
-                        "                    [--dry-run] [--quiet]\n");
+                        "                    [--dry-run] [--sort-rows] [--quiet]\n");
             std::exit(0);
         } else {
             throw std::runtime_error("unknown argument '" + k + "'");
@@ -372,8 +375,9 @@ int run(int argc, char** argv) {
             // prepare_sim_inputs (simulation.cpp:140-158): read the matrix, its QBER grid
             for (auto& d : dev) {
                 qkd_status st = QKD_OK;
-                d.code = cfg.USE_DENSE_MATRICES ? qkd_code_from_dense(path.c_str(), d.index, &st)
-                                                : qkd_code_from_alist(path.c_str(), d.index, &st);
+                d.code = cfg.USE_DENSE_MATRICES
+                             ? qkd_code_from_dense(path.c_str(), d.index, &st)
+                             : qkd_code_from_alist_ex(path.c_str(), d.index, args.sort_rows ? QKD_READ_SORT_ROWS : 0u, &st);
                 if (!d.code) fail("cannot read matrix " + path.string());
                 d.ws = qkd_workspace_create(d.code, &st);
                 if (!d.ws) fail("qkd_workspace_create");

@@ -127,6 +127,13 @@ QKD_API qkd_code *qkd_code_create(int32_t n_bits, int32_t n_checks, const int32_
  * non-zero counts per line, 1-based entries, the first `weight` entries
  * of each line). */
 QKD_API qkd_code *qkd_code_from_alist(const char *path, int device, qkd_status *status);
+/* Reader options (reader hardening). QKD_READ_SORT_ROWS: sort
+ * every bit and check line before validation, so a file whose rows are not
+ * ascending is read as the matrix it describes (default: QKD_ERR_UNSORTED,
+ * where the reference would silently mis-route messages, §8(a) A1). */
+#define QKD_READ_SORT_ROWS 0x1u
+QKD_API qkd_code *qkd_code_from_alist_ex(const char *path, int device, uint32_t read_flags,
+                                         qkd_status *status);
 /* Reads a dense 0/1 matrix file (one row per line). */
 QKD_API qkd_code *qkd_code_from_dense(const char *path, int device, qkd_status *status);
 QKD_API void qkd_code_destroy(qkd_code *code);

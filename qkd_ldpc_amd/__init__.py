@@ -106,8 +106,11 @@ class HMatrix:
         return cls(h)
 
     @classmethod
-    def from_alist(cls, path: str, device: int = 0) -> "HMatrix":
-        return cls._make(N.lib().qkd_code_from_alist, str(path).encode(), device)
+    def from_alist(cls, path: str, device: int = 0, sort_rows: bool = False) -> "HMatrix":
+        """read_sparse_alist_matrix. sort_rows: accept lines that are not ascending
+        by sorting them (QKD_READ_SORT_ROWS) instead of rejecting the file."""
+        return cls._make(N.lib().qkd_code_from_alist_ex, str(path).encode(), device,
+                         N.READ_SORT_ROWS if sort_rows else 0)
 
     @classmethod
     def from_dense(cls, path: str, device: int = 0) -> "HMatrix":

@@ -35,6 +35,7 @@ ERR_IO = 7
 ERR_UNSUPPORTED = 8
 
 FLAG_THRESHOLD = 0x1
+READ_SORT_ROWS = 0x1   # qkd_code_from_alist_ex
 # decoder variants (include/qkd_ldpc.h: QKD_VARIANT_*)
 VARIANTS = {"sp_f64": 0x00, "sp_f32": 0x10, "minsum": 0x20}
 MINSUM_SCALE_SHIFT = 8
@@ -48,6 +49,7 @@ EXPORTS = [
     "qkd_workspace_destroy", "qkd_syndrome_batch", "qkd_decode_batch", "qkd_qkd_ldpc_batch",
     "qkd_keygen_batch", "qkd_trials_batch", "qkd_counters_batch", "qkd_make_seeds",
     "qkd_qber_range", "qkd_debug_phase_cycles", "qkd_debug_math", "qkd_trace_decode",
+    "qkd_code_from_alist_ex",
 ]
 
 
@@ -94,6 +96,7 @@ def lib():
             "qkd_device_count": (C.c_int, []),
             "qkd_code_create": (P, [I32, I32, P, P, C.c_int, C.POINTER(st)]),
             "qkd_code_from_alist": (P, [C.c_char_p, C.c_int, C.POINTER(st)]),
+            "qkd_code_from_alist_ex": (P, [C.c_char_p, C.c_int, U32, C.POINTER(st)]),
             "qkd_code_from_dense": (P, [C.c_char_p, C.c_int, C.POINTER(st)]),
             "qkd_code_destroy": (None, [P]),
             "qkd_code_get_info": (st, [P, C.POINTER(CodeInfo)]),

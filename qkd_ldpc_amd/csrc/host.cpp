@@ -255,8 +255,12 @@ static bool read_lines(const char* path, std::vector<std::vector<long>>& rows) {
 }
 
 // read_sparse_alist_matrix (reference array_and_matrix_operations.cpp:109-292)
+// sort_rows (QKD_READ_SORT_ROWS): each line's entries are sorted first, so a
+// file whose rows are not ascending is read as the matrix it describes instead
+// of being rejected (the reference would silently pair messages with the
+// wrong edges).
 static qkd_status parse_alist(const char* path, int32_t& n, int32_t& m, std::vector<int32_t>& cptr,
-                              std::vector<int32_t>& cidx) {
+                              std::vector<int32_t>& cidx, bool sort_rows) {
     std::vector<std::vector<long>> v;
     if (!path || !read_lines(path, v))
         return set_error(QKD_ERR_IO, "Failed to open file: %s", path ? path : "(null)");
@@ -287,6 +291,7 @@ static qkd_status parse_alist(const char* path, int32_t& n, int32_t& m, std::vec
     for (int32_t j = 0; j < m; ++j) {
         const auto& L = v[4 + nb + j];
         for (long k = 0; k < v[3][j]; ++k) cidx.push_back((int32_t)(L[k] - 1));
+        if (sort_rows) std::sort(cidx.begin() + cptr[j], cidx.end());
         cptr[j + 1] = (int32_t)cidx.size();
     }
     // bit_nodes rows must describe the same edge set (the reference reads
@@ -303,6 +308,7 @@ static qkd_status parse_alist(const char* path, int32_t& n, int32_t& m, std::vec
         const auto& L = v[4 + i];
         std::vector<int32_t> row;
         for (long k = 0; k < v[2][i]; ++k) row.push_back((int32_t)(L[k] - 1));
+        if (sort_rows) std::sort(row.begin(), row.end());
         if (row != from_checks[i]) {
             std::vector<int32_t> s = row;
             std::sort(s.begin(), s.end());
@@ -386,10 +392,19 @@ qkd_code* qkd_code_create(int32_t n_bits, int32_t n_checks, const int32_t* check
 }
 
 qkd_code* qkd_code_from_alist(const char* path, int device, qkd_status* status) {
+    return qkd_code_from_alist_ex(path, device, 0, status);
+}
+
+qkd_code* qkd_code_from_alist_ex(const char* path, int device, uint32_t read_flags, qkd_status* status) {
     clear_error();
+    if (read_flags & ~QKD_READ_SORT_ROWS) {
+        set_error(QKD_ERR_INVALID_ARG, "unknown read flags 0x%x", read_flags);
+        if (status) *status = QKD_ERR_INVALID_ARG;
+        return nullptr;
+    }
     int32_t n = 0, m = 0;
     std::vector<int32_t> cptr, cidx;
-    qkd_status s = parse_alist(path, n, m, cptr, cidx);
+    qkd_status s = parse_alist(path, n, m, cptr, cidx, (read_flags & QKD_READ_SORT_ROWS) != 0);
     if (s != QKD_OK) {
         if (status) *status = s;
         return nullptr;

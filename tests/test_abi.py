@@ -135,6 +135,45 @@ def test_alist_reader_accepts_reference_layout(N, golden_code, tmp_path):
         assert st == N.OK, msg
 
 
+def _alist_status_ex(N, path, flags):
+    st = C.c_int(-1)
+    h = N.lib().qkd_code_from_alist_ex(path.encode(), 0, flags, C.byref(st))
+    if h:
+        N.lib().qkd_code_destroy(h)
+    return st.value, N.last_error()
+
+
+def _parsed(N, st):
+    """Parsed and validated: OK with a GPU, the device error without one."""
+    return st == (N.ERR_DEVICE if N.lib().qkd_device_count() == 0 else N.OK)
+
+
+def test_alist_reader_sort_rows_option(N, tmp_path):
+    """QKD_READ_SORT_ROWS reads a file whose lines are not ascending as the matrix it
+    describes; without it the file is rejected (the reference mis-routes, A1)."""
+    p = tmp_path / "u.txt"
+    p.write_text("4 2\n2 4\n2 2 2 2\n4 4\n2 1\n1 2\n1 2\n1 2\n4 3 2 1\n1 2 3 4\n")
+    assert _alist_status_ex(N, str(p), 0)[0] == N.ERR_UNSORTED
+    st, msg = _alist_status_ex(N, str(p), N.READ_SORT_ROWS)
+    assert _parsed(N, st), msg
+    # sorting does not excuse a wrong edge set
+    p.write_text("4 2\n2 4\n2 2 2 2\n4 4\n2 1\n1 2\n1 2\n1 1\n4 3 2 1\n1 2 3 4\n")
+    assert _alist_status_ex(N, str(p), N.READ_SORT_ROWS)[0] == N.ERR_BAD_CODE
+    assert _alist_status_ex(N, str(p), 0x80)[0] == N.ERR_INVALID_ARG
+
+
+def test_alist_reader_line_endings_and_blank_tail(N, golden_code, tmp_path):
+    """CRLF line endings and trailing blank lines (files edited on other systems)."""
+    g = golden_code
+    p = str(tmp_path / "c.alist")
+    write_alist(p, 10240, 5231, g["bit_off"], g["bit_idx"], g["chk_off"], g["chk_idx"], pad=False)
+    text = open(p).read().replace("\n", "\r\n") + "\r\n\r\n"
+    with open(p, "w", newline="") as f:
+        f.write(text)
+    st, msg = _alist_status(N, p)
+    assert _parsed(N, st), msg
+
+
 def test_dense_reader_errors(N, tmp_path):
     def status(text):
         p = tmp_path / "d.txt"
