@@ -188,8 +188,8 @@ struct DecodeLds {
 
 // Bit phase: message rows per bit loaded ahead of the ordered sum, and rounds
 // (bits tid + r*kDecodeBlock) per load batch.
-constexpr int kDvUnroll = 4;
-constexpr int kBitChunk = 4;
+constexpr int kDvUnroll = 3;
+constexpr int kBitChunk = 5;
 // Plan-walking loops outside the check phase load this many tasks' plan words
 // per trip (the plan carries kPlanPadTasks >= kPlanGroup * NW idle tasks).
 constexpr int kPlanGroup = 4;
