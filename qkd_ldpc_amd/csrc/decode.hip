@@ -107,6 +107,10 @@ struct DecodeArgs {
     // c2b store (max_dv x n_pad) then the bit totals (n_pad), or nullptr
     double* trace;
     size_t trace_stride;
+    // large codes (decode_kernel<..., GT = true>): the bit totals of each
+    // workgroup's frame in global scratch, totals_stride doubles apart
+    double* totals;
+    size_t totals_stride;
 };
 
 // Phase-clock accumulation (diagnostic; a wave-uniform test when off). Each
@@ -166,10 +170,13 @@ __host__ __device__ inline int decode_m_words(int m) { return ((m + 63) / 64) * 
 //   cst    [m] (uint4)      kRuleMinSumLds: per-check min-sum state (ms_state)
 struct DecodeLds {
     size_t tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, cst, bytes;
-    __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries, int esz,
-                                  int cst_checks = 0) {
+    // total_esz: bytes per bit total in LDS (0: the totals live in global
+    // memory, large codes)
+    __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries, int total_esz,
+                                  int cst_checks = 0, int row_esz = 0) {
         const int m_words = decode_m_words(m);
-        tsyn = ((size_t)n_pad * esz + 15) & ~(size_t)15;
+        const int esz = row_esz ? row_esz : total_esz;
+        tsyn = ((size_t)n_pad * total_esz + 15) & ~(size_t)15;
         xsyn = tsyn + (size_t)m_words * 4;
         qsyn = xsyn + (size_t)m_words * 4;
         tval = (qsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
@@ -195,12 +202,13 @@ constexpr int kBitChunk = 5;
 constexpr int kPlanGroup = 4;
 
 // ---- wave-plan words (qkd_plan.h) ------------------------------------------
-__device__ __forceinline__ uint32_t pw_bit(uint32_t w) { return w & qkdp::kPlanBitMask; }
-__device__ __forceinline__ uint32_t pw_row(uint32_t w) { return (w >> 15) & 31u; }
-__device__ __forceinline__ int pw_start(uint32_t w) { return (int)((w >> 20) & 63u); }
-__device__ __forceinline__ int pw_deg(uint32_t w) { return (int)(w >> 26) + 1; }
+__device__ __forceinline__ uint32_t pw_bit(uint2 p) { return p.x & qkdp::kPlanBitMask; }
+__device__ __forceinline__ uint32_t pw_row(uint2 p) { return p.x >> 24; }
+__device__ __forceinline__ uint32_t pw_chk(uint2 p) { return p.y & qkdp::kPlanChkMask; }
+__device__ __forceinline__ int pw_start(uint2 p) { return (int)((p.y >> 20) & 63u); }
+__device__ __forceinline__ int pw_deg(uint2 p) { return (int)(p.y >> 26) + 1; }
 // Parity of the lanes of this lane's check (its segment) in a wave ballot.
-__device__ __forceinline__ int seg_parity(uint64_t ballot, uint32_t w) {
+__device__ __forceinline__ int seg_parity(uint64_t ballot, uint2 w) {
     const int deg = pw_deg(w);
     const uint64_t m = deg == 64 ? ~0ull : ((1ull << deg) - 1ull);
     return __popcll(ballot & (m << pw_start(w))) & 1;
@@ -265,7 +273,7 @@ __device__ __forceinline__ T edge_in(T x, T old, T thr) {
 // (segment [start, start + deg) of `row`; the row has 64 + DC entries, so reads
 // past a segment's end stay inside it and are discarded).
 template <bool CLAMP, int DC, int RULE, typename T>
-__device__ __forceinline__ T edge_out(T tv, uint32_t w, uint32_t sbit, int lane, T thr, const T* row,
+__device__ __forceinline__ T edge_out(T tv, uint2 w, uint32_t sbit, int lane, T thr, const T* row,
                                       float ms_scale) {
     const int start = pw_start(w);
     const int deg = pw_deg(w);
@@ -343,24 +351,27 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
     if (t >= n_tasks) return;
     const uint2* pl = plan + lane;
 #ifdef QKD_EXP_MSG_LOCAL
-    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + lane + 64 * (wave & 7); };
+    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p) * n_pad + lane + 64 * (wave & 7); };
 #elif defined(QKD_EXP_MSG_SMALL)
-    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + (pw_bit(p.x) & 511); };
+    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p) * n_pad + (pw_bit(p) & 511); };
 #else
-    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p.x) * n_pad + pw_bit(p.x); };
+    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p) * n_pad + pw_bit(p); };
 #endif
     // the incoming value: a bit total, or (kSrcTable) the tabulated tanh
     auto src = [&](uint2 p) -> T {
-        if constexpr (SRC == kSrcTable) return tab2[t2idx[pw_bit(p.x)] + pw_row(p.x)];
-        else return total[pw_bit(p.x)];
+        if constexpr (SRC == kSrcTable) return tab2[t2idx[pw_bit(p)] + pw_row(p)];
+        else return total[pw_bit(p)];
     };
     // the target syndrome bit of the lane's check
-    auto sbit = [&](uint2 p) -> uint32_t { return (tsyn[p.y >> 5] >> (p.y & 31)) & 1u; };
+    auto sbit = [&](uint2 p) -> uint32_t {
+        const uint32_t j = pw_chk(p);
+        return (tsyn[j >> 5] >> (j & 31)) & 1u;
+    };
     auto edge = [&](T x, T o, uint2 w) -> T {
         const T a = edge_in<SRC, CLAMP, RULE>(x, o, thr);
         row[lane] = a;
         wave_lds_sync();
-        return edge_out<CLAMP, DC, RULE>(a, w.x, sbit(w), lane, thr, row, ms_scale);
+        return edge_out<CLAMP, DC, RULE>(a, w, sbit(w), lane, thr, row, ms_scale);
     };
     uint2 wa = pl[t * 64];
     uint2 wb = pl[(t + NW) * 64];
@@ -551,11 +562,12 @@ __device__ __forceinline__ void first_check_phase(const uint2* __restrict__ plan
         for (int u = 0; u < kPlanGroup; ++u) {
             const int t = t0 + u * NW;
             if (t >= n_tasks) break;
-            const uint32_t bit = pw_bit(w[u].x);
+            const uint32_t bit = pw_bit(w[u]);
+            const uint32_t j = pw_chk(w[u]);
             const uint32_t sg = (uint32_t)qkdm::hi32(total[bit]) >> 31;
-            const uint32_t sp = ((tsyn[w[u].y >> 5] >> (w[u].y & 31)) & 1u) ^ (uint32_t)seg_parity(__ballot(sg), w[u].x);
-            const double cm = ctab[pw_deg(w[u].x)];
-            c2b[pw_row(w[u].x) * n_pad + bit] = (sp ^ sg) ? -cm : cm;
+            const uint32_t sp = ((tsyn[j >> 5] >> (j & 31)) & 1u) ^ (uint32_t)seg_parity(__ballot(sg), w[u]);
+            const double cm = ctab[pw_deg(w[u])];
+            c2b[pw_row(w[u]) * n_pad + bit] = (sp ^ sg) ? -cm : cm;
         }
     }
 }
@@ -580,19 +592,29 @@ __device__ __forceinline__ void first_check_phase(const uint2* __restrict__ plan
 //    hard decision z_i = total_i <= 0; if z_i, XOR it into the syndrome bit of
 //    each of its checks (LDS bit array; XOR is order-free, so exact)
 //  syndrome test (:277-285): compare with the target words, block-wide any()
-template <int MODE, int RULE, int DC, bool CLAMP>
+//
+// GT (large codes, N beyond what LDS holds): the bit totals live in global
+// scratch instead of LDS; everything else is the same kernel. The tables of
+// the QKD path (per-bit LDS indices) and the LDS-state min-sum are not used.
+template <int MODE, int RULE, int DC, bool CLAMP, bool GT>
 __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     using T = typename RuleMsg<RULE>::T;
     // the exact QKD-path shortcuts (first/second-iteration tables) exist for
     // the reference rule only
-    constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
+    constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64 && !GT;
     constexpr bool MSL = RULE == kRuleMinSumLds;
+    static_assert(!(MSL && GT), "the LDS-state min-sum keeps its totals in LDS");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
-    const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries, (int)sizeof(T), MSL ? c.m : 0);
+    const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries, GT ? 0 : (int)sizeof(T),
+                      MSL ? c.m : 0, (int)sizeof(T));
     uint4* cst = reinterpret_cast<uint4*>(smem + L.cst);
     const int m_words = decode_m_words(c.m);
-    T* total = reinterpret_cast<T*>(smem);
+    T* total;
+    if constexpr (GT)
+        total = reinterpret_cast<T*>(a.totals + (size_t)blockIdx.x * a.totals_stride);
+    else
+        total = reinterpret_cast<T*>(smem);
     uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
     uint32_t* qsyn = reinterpret_cast<uint32_t*>(smem + L.qsyn);
@@ -645,6 +667,9 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
         }
         // ---- prologue: channel LLRs into LDS (:188 / :400-405); the dummy
         //      column n of idle plan lanes gets 0
+        // Bob's bits of this thread's bit-phase rounds (round r: bit tid + r *
+        // kDecodeBlock), N <= 32 * kDecodeBlock; the large-code kernels read
+        // them from the packed key instead (any N)
         uint32_t bobmask = 0;
         {
             int r = 0;
@@ -654,7 +679,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     l = (T)a.llr[(size_t)f * c.n + i];
                 } else {
                     const uint32_t bb = (uint32_t)((sw[a.words + (i >> 6)] >> (i & 63)) & 1u);
-                    bobmask |= bb << r;
+                    if (!GT) bobmask |= bb << r;
                     l = bb ? -llr_p : llr_p;
                 }
                 total[i] = l;
@@ -785,7 +810,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     const int deg = dg[u];
                     T acc;
                     if (MODE == kModeLlr) acc = (T)a.llr[(size_t)f * c.n + i];
-                    else acc = ((bobmask >> r) & 1u) ? -llr_p : llr_p;
+                    else if constexpr (GT)
+                        acc = ((a.bob_w[(size_t)f * a.words + (i >> 6)] >> (i & 63)) & 1u) ? -llr_p : llr_p;
+                    else
+                        acc = ((bobmask >> r) & 1u) ? -llr_p : llr_p;
                     if constexpr (TABLES) if (fold1 && it == 0) {
                         // fold_first_message: message of the k-th check j of bit i is
                         // +-C_{d_j} with sign = sign(P_j) ^ sign(LLR_i) (first_check_phase)
@@ -1145,37 +1173,48 @@ __global__ void counters_init_kernel(qkd_counters* c) {
 using DecodeFn = void (*)(DecodeArgs);
 
 // Check-degree buckets: the in-check product reads DC values per lane.
-template <int MODE, int RULE, bool CLAMP>
+template <int MODE, int RULE, bool CLAMP, bool GT>
 static DecodeFn pick_decode_dc(int max_dc, int* dc) {
-    if (max_dc <= 4) { *dc = 4; return decode_kernel<MODE, RULE, 4, CLAMP>; }
-    if (max_dc <= 6) { *dc = 6; return decode_kernel<MODE, RULE, 6, CLAMP>; }
-    if (max_dc <= 8) { *dc = 8; return decode_kernel<MODE, RULE, 8, CLAMP>; }
-    if (max_dc <= 16) { *dc = 16; return decode_kernel<MODE, RULE, 16, CLAMP>; }
-    if constexpr (RULE == kRuleMinSumLds) {       // decode_ms_fits: degree <= 32
-        *dc = 32;
-        return decode_kernel<MODE, RULE, 32, CLAMP>;
-    } else {
+    if constexpr (GT) {                           // large codes: two buckets
+        if (max_dc <= 16) { *dc = 16; return decode_kernel<MODE, RULE, 16, CLAMP, true>; }
         *dc = 64;
-        return decode_kernel<MODE, RULE, 64, CLAMP>;
+        return decode_kernel<MODE, RULE, 64, CLAMP, true>;
+    } else {
+        if (max_dc <= 4) { *dc = 4; return decode_kernel<MODE, RULE, 4, CLAMP, false>; }
+        if (max_dc <= 6) { *dc = 6; return decode_kernel<MODE, RULE, 6, CLAMP, false>; }
+        if (max_dc <= 8) { *dc = 8; return decode_kernel<MODE, RULE, 8, CLAMP, false>; }
+        if (max_dc <= 16) { *dc = 16; return decode_kernel<MODE, RULE, 16, CLAMP, false>; }
+        if constexpr (RULE == kRuleMinSumLds) {   // decode_ms_fits: degree <= 32
+            *dc = 32;
+            return decode_kernel<MODE, RULE, 32, CLAMP, false>;
+        } else {
+            *dc = 64;
+            return decode_kernel<MODE, RULE, 64, CLAMP, false>;
+        }
     }
 }
 
-template <int MODE, int RULE>
+template <int MODE, int RULE, bool GT>
 static DecodeFn pick_decode_clamp(bool clamp, int max_dc, int* dc) {
-    return clamp ? pick_decode_dc<MODE, RULE, true>(max_dc, dc) : pick_decode_dc<MODE, RULE, false>(max_dc, dc);
+    return clamp ? pick_decode_dc<MODE, RULE, true, GT>(max_dc, dc)
+                 : pick_decode_dc<MODE, RULE, false, GT>(max_dc, dc);
 }
 
-template <int MODE>
+template <int MODE, bool GT>
 static DecodeFn pick_decode_rule(int rule, bool clamp, int max_dc, int* dc) {
-    if (rule == kRuleSp32) return pick_decode_clamp<MODE, kRuleSp32>(clamp, max_dc, dc);
-    if (rule == kRuleMinSum) return pick_decode_clamp<MODE, kRuleMinSum>(clamp, max_dc, dc);
-    if (rule == kRuleMinSumLds) return pick_decode_clamp<MODE, kRuleMinSumLds>(clamp, max_dc, dc);
-    return pick_decode_clamp<MODE, kRuleSp64>(clamp, max_dc, dc);
+    if (rule == kRuleSp32) return pick_decode_clamp<MODE, kRuleSp32, GT>(clamp, max_dc, dc);
+    if (rule == kRuleMinSum) return pick_decode_clamp<MODE, kRuleMinSum, GT>(clamp, max_dc, dc);
+    if constexpr (!GT)
+        if (rule == kRuleMinSumLds) return pick_decode_clamp<MODE, kRuleMinSumLds, false>(clamp, max_dc, dc);
+    return pick_decode_clamp<MODE, kRuleSp64, GT>(clamp, max_dc, dc);
 }
 
-static DecodeFn pick_decode(int mode, int rule, bool clamp, int max_dc, int* dc) {
-    return mode == kModeLlr ? pick_decode_rule<kModeLlr>(rule, clamp, max_dc, dc)
-                            : pick_decode_rule<kModeKeys>(rule, clamp, max_dc, dc);
+static DecodeFn pick_decode(int mode, int rule, bool clamp, int max_dc, bool gt, int* dc) {
+    if (gt)
+        return mode == kModeLlr ? pick_decode_rule<kModeLlr, true>(rule, clamp, max_dc, dc)
+                                : pick_decode_rule<kModeKeys, true>(rule, clamp, max_dc, dc);
+    return mode == kModeLlr ? pick_decode_rule<kModeLlr, false>(rule, clamp, max_dc, dc)
+                            : pick_decode_rule<kModeKeys, false>(rule, clamp, max_dc, dc);
 }
 
 static int rule_of(uint32_t flags) {
@@ -1191,16 +1230,27 @@ static float minsum_scale_of(uint32_t flags) {
     return q ? (float)q / 256.0f : (float)QKD_MINSUM_DEFAULT_SCALE;
 }
 
-static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries, int rule) {
-    return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries, rule == kRuleSp64 ? 8 : 4,
-                     rule == kRuleMinSumLds ? c->m : 0).bytes;
+static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries, int rule, bool gt = false) {
+    const int esz = rule == kRuleSp64 ? 8 : 4;
+    return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries, gt ? 0 : esz,
+                     rule == kRuleMinSumLds ? c->m : 0, esz).bytes;
+}
+
+static constexpr size_t kLdsBytesMax = 160 * 1024;
+
+static int dc_bucket(int max_dc) {
+    return max_dc <= 4 ? 4 : max_dc <= 6 ? 6 : max_dc <= 8 ? 8 : max_dc <= 16 ? 16 : 64;
+}
+
+// Totals in LDS unless the code is too long for them (the large-code kernels).
+static bool decode_needs_gt(const qkd_code* c, int rule, int tab2_entries) {
+    return c->n > kMaxBitsLds || decode_lds_bytes(c, dc_bucket(c->max_dc), tab2_entries, rule) > kLdsBytesMax;
 }
 
 // The LDS-resident min-sum needs the check state (sign bits in one word:
 // degree <= 32) and all of its LDS in one workgroup.
-static constexpr size_t kLdsBytesMax = 160 * 1024;
 static bool decode_ms_fits(const qkd_code* c) {
-    if (c->max_dc > 32) return false;
+    if (c->max_dc > 32 || c->n > kMaxBitsLds) return false;
     const int dc = c->max_dc <= 4 ? 4 : c->max_dc <= 6 ? 6 : c->max_dc <= 8 ? 8 : c->max_dc <= 16 ? 16 : 32;
     return decode_lds_bytes(c, dc, 0, kRuleMinSumLds) <= kLdsBytesMax;
 }
@@ -1222,7 +1272,9 @@ qkd_status ws_reserve_decode(qkd_workspace* ws, size_t slots) {
     if (ws->c2b) QKD_HIP(hipFree(ws->c2b));
     ws->c2b = nullptr;
     ws->c2b_slots = 0;
-    const size_t bytes = slots * (size_t)c->max_dv * c->n_pad * sizeof(double);
+    // per slot: the c2b store (max_dv rows) and, at the end, a total row
+    // (large codes keep their bit totals there)
+    const size_t bytes = slots * ((size_t)c->max_dv + 1) * c->n_pad * sizeof(double);
     if (hipMalloc(&ws->c2b, bytes) != hipSuccess)
         return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate %zu B of c2b scratch", bytes);
     ws->c2b_slots = slots;
@@ -1302,8 +1354,13 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     const bool ms_global = ms_store && !strcmp(ms_store, "global");
     if (rule == kRuleMinSum && !ms_global && decode_ms_fits(c)) rule = kRuleMinSumLds;
     a.ms_scale = minsum_scale_of(flags);
-    DecodeFn fn = pick_decode(mode, rule, a.clamp_on != 0, c->max_dc, &dc);
-    const size_t lds = decode_lds_bytes(c, dc, a.tab2_entries, rule);
+    const bool gt = decode_needs_gt(c, rule, a.tab2_entries);
+    if (gt) {                                     // large code: no per-bit LDS tables
+        a.first_table = 0;
+        a.tab2_entries = 0;
+    }
+    DecodeFn fn = pick_decode(mode, rule, a.clamp_on != 0, c->max_dc, gt, &dc);
+    const size_t lds = decode_lds_bytes(c, dc, a.tab2_entries, rule, gt);
     int grid = 0;
     qkd_status s = decode_grid(c, fn, lds, &grid);
     if (s != QKD_OK) return s;
@@ -1313,6 +1370,9 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     a.code = c->view();
     a.c2b = ws->c2b;
     a.c2b_stride = (size_t)c->max_dv * c->n_pad;
+    // the workspace holds one total row per slot after all the message stores
+    a.totals = gt ? ws->c2b + ws->c2b_slots * a.c2b_stride : nullptr;
+    a.totals_stride = c->n_pad;
     a.counter = ws->counter;
     QKD_HIP(hipMemsetAsync(ws->counter, 0, 4, stream));
     static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;

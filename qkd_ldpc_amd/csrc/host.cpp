@@ -89,10 +89,10 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         return set_error(QKD_ERR_UNSUPPORTED, "check degree %d exceeds %d", max_dc, kMaxCheckDegree);
     if (max_dv > qkdp::kPlanMaxBitDegree)
         return set_error(QKD_ERR_UNSUPPORTED, "bit degree %d exceeds %d", max_dv, qkdp::kPlanMaxBitDegree);
-    if (n > qkdp::kPlanMaxBits)
-        return set_error(QKD_ERR_UNSUPPORTED, "N=%d exceeds the plan limit %d", n, qkdp::kPlanMaxBits);
-    if (n > kMaxBitsLds)
-        return set_error(QKD_ERR_UNSUPPORTED, "N=%d exceeds the LDS-resident limit %d", n, kMaxBitsLds);
+    if (n >= qkdp::kPlanMaxBits)
+        return set_error(QKD_ERR_UNSUPPORTED, "N=%d exceeds the plan limit %d", n, qkdp::kPlanMaxBits - 1);
+    if (m > qkdp::kPlanMaxChecks)
+        return set_error(QKD_ERR_UNSUPPORTED, "M=%d exceeds the plan limit %d", m, qkdp::kPlanMaxChecks);
 
     c->device = device;
     c->n = n;
@@ -194,8 +194,7 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         QKD_HIP(hipMemcpy(c->d_pat_deg, c->pat_deg.data(), c->pat_deg.size(), hipMemcpyHostToDevice));
     }
     std::vector<uint2> plan2(plan.word.size());
-    for (size_t k = 0; k < plan.word.size(); ++k)
-        plan2[k] = make_uint2(plan.word[k], plan.chk[k] < 0 ? 0u : (uint32_t)plan.chk[k]);
+    for (size_t k = 0; k < plan.word.size(); ++k) plan2[k] = make_uint2(plan.word[k], plan.seg[k]);
     QKD_HIP(hipMalloc(&c->d_plan, plan2.size() * sizeof(uint2)));
     QKD_HIP(hipMemcpy(c->d_plan, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
     // Key-generation jump-ahead: chunk = draws per lane, a multiple of 64 so

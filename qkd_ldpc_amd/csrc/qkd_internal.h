@@ -35,8 +35,8 @@ constexpr uint32_t kKeygenFastMaxErrors = 4096;
 //   chk_bits[k * m_pad + j]  bit index of slot k of check j (ascending), -1 pad
 //                            (thread-per-check syndrome kernel)
 //   plan[s]                  the check-phase wave plan (qkd_plan.h): slot
-//                            s = task*64 + lane holds one edge: {plan word,
-//                            check index}
+//                            s = task*64 + lane holds one edge: {bit | row,
+//                            check | segment start | degree} (qkd_plan.h)
 //   bit_chk[k * n_pad + i]   k-th check of bit i (ascending), -1 pad
 //   bit_pos[k * n_pad + i]   position of bit i in that check's ascending row
 //                            (LDS min-sum state lookups)
@@ -49,7 +49,7 @@ struct DeviceCode {
     int32_t n_tasks;
     const int32_t* chk_bits;
     const uint8_t* chk_deg;
-    const uint2* plan;            // {plan word, check index (0 on idle lanes)}
+    const uint2* plan;            // {bit | row << 24, check | start << 20 | (deg-1) << 26}
     const int32_t* bit_chk;
     const uint8_t* bit_pos;
     const uint8_t* bit_deg;

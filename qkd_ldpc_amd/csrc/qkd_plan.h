@@ -22,12 +22,13 @@
 // else reads, so the hot loop needs no idle-lane branches. Their plan_chk
 // entry is -1.
 //
-// Packed plan word of a lane (uint32):
-//   bits  0..14  bit index i of the edge (N = the dummy column on an idle lane)
-//   bits 15..19  position of the check among bit i's checks (ascending), i.e.
-//                the row of the bit-major message store c2b[k][i]
-//   bits 20..25  first lane of the segment (the check's first edge)
-//   bits 26..31  degree - 1 of the check
+// Packed plan entry of a lane (two uint32 words, the kernels' uint2):
+//   word  bits  0..23  bit index i of the edge (N = the dummy column on an idle lane)
+//         bits 24..28  position of the check among bit i's checks (ascending), i.e.
+//                      the row of the bit-major message store c2b[k][i]
+//   seg   bits  0..19  check index j (0 on an idle lane)
+//         bits 20..25  first lane of the segment (the check's first edge)
+//         bits 26..31  degree - 1 of the check
 #pragma once
 #include <stdint.h>
 
@@ -36,19 +37,23 @@
 
 namespace qkdp {
 
-constexpr uint32_t kPlanBitMask = 0x7FFFu;
+constexpr uint32_t kPlanBitMask = 0xFFFFFFu;
+constexpr uint32_t kPlanChkMask = 0xFFFFFu;
 constexpr int kPlanMaxBits = (int)kPlanBitMask;    // N must be < this (dummy column N)
+constexpr int kPlanMaxChecks = (int)kPlanChkMask + 1;
 constexpr int kPlanPadTasks = 128;                 // idle tasks appended to the plan
 constexpr int kPlanMaxDegree = 64;                 // check degree: one wavefront
 constexpr int kPlanMaxBitDegree = 32;              // bit degree: 5-bit row index
 
-inline uint32_t plan_word(uint32_t bit, uint32_t krow, uint32_t start, uint32_t deg) {
-    return bit | (krow << 15) | (start << 20) | ((deg - 1) << 26);
+inline uint32_t plan_word(uint32_t bit, uint32_t krow) { return bit | (krow << 24); }
+inline uint32_t plan_seg(uint32_t chk, uint32_t start, uint32_t deg) {
+    return chk | (start << 20) | ((deg - 1) << 26);
 }
 
 struct WavePlan {
     int32_t n_tasks = 0;                 // real tasks; word/chk hold n_tasks + kPlanPadTasks
-    std::vector<uint32_t> word;          // [n_tasks*64]
+    std::vector<uint32_t> word;          // [n_tasks*64] bit | row << 24
+    std::vector<uint32_t> seg;           // [n_tasks*64] check | start << 20 | (deg-1) << 26
     std::vector<int32_t> chk;            // [n_tasks*64] check of the slot, -1 idle
     std::vector<int32_t> slot_of_edge;   // [E] plan slot of check-CSR edge k
 };
@@ -58,7 +63,8 @@ struct WavePlan {
 // list). Degrees must be in [1, 64]. Returns false if a degree is out of range.
 inline bool build_wave_plan(int32_t n, int32_t m, const int32_t* cptr, const int32_t* cidx,
                             const int32_t* krow, WavePlan& p) {
-    const uint32_t idle = plan_word((uint32_t)n, 0, 0, 1);
+    const uint32_t idle = plan_word((uint32_t)n, 0);
+    const uint32_t idle_seg = plan_seg(0, 0, 1);
     // degree classes, largest first; checks of a class in ascending order
     std::vector<std::vector<int32_t>> by_deg(kPlanMaxDegree + 1);
     for (int32_t j = 0; j < m; ++j) {
@@ -73,6 +79,7 @@ inline bool build_wave_plan(int32_t n, int32_t m, const int32_t* cptr, const int
     const int nc = (int)degs.size();
     const int cap = 64;
     p.word.clear();
+    p.seg.clear();
     p.chk.clear();
     p.slot_of_edge.assign(cptr[m], -1);
     int32_t left = m;
@@ -107,6 +114,7 @@ inline bool build_wave_plan(int32_t n, int32_t m, const int32_t* cptr, const int
         }
         const int32_t task = p.n_tasks++;
         p.word.resize((size_t)p.n_tasks * 64, idle);
+        p.seg.resize((size_t)p.n_tasks * 64, idle_seg);
         p.chk.resize((size_t)p.n_tasks * 64, -1);
         int lane = 0;
         for (int i = 0; i < nc; ++i) {
@@ -116,8 +124,8 @@ inline bool build_wave_plan(int32_t n, int32_t m, const int32_t* cptr, const int
                 --left;
                 for (int k = 0; k < d; ++k) {
                     const size_t slot = (size_t)task * 64 + lane + k;
-                    p.word[slot] = plan_word((uint32_t)cidx[cptr[j] + k], (uint32_t)krow[cptr[j] + k],
-                                             (uint32_t)lane, (uint32_t)d);
+                    p.word[slot] = plan_word((uint32_t)cidx[cptr[j] + k], (uint32_t)krow[cptr[j] + k]);
+                    p.seg[slot] = plan_seg((uint32_t)j, (uint32_t)lane, (uint32_t)d);
                     p.chk[slot] = j;
                     p.slot_of_edge[cptr[j] + k] = (int32_t)slot;
                 }
@@ -126,6 +134,7 @@ inline bool build_wave_plan(int32_t n, int32_t m, const int32_t* cptr, const int
         }
     }
     p.word.resize((size_t)(p.n_tasks + kPlanPadTasks) * 64, idle);
+    p.seg.resize((size_t)(p.n_tasks + kPlanPadTasks) * 64, idle_seg);
     p.chk.resize((size_t)(p.n_tasks + kPlanPadTasks) * 64, -1);
     return true;
 }

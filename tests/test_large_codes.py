@@ -1,0 +1,126 @@
+"""Codes longer than the LDS-resident totals allow (N > 20480): the same decoder
+with its bit totals in global scratch (decode_kernel<..., GT = true>). Random
+regular (3, 6) codes; parity with the oracle bit for bit, fused trials
+included (both key generators: the jump-ahead one for floor(N q) <= 4096 and
+the serial one beyond)."""
+import numpy as np
+import pytest
+
+from conftest import write_alist
+
+
+def regular_code(n, dv=3, dc=6, seed=0):
+    """Random (dv, dc)-regular parity-check matrix without repeated edges, as
+    check rows (ascending) -> (check_ptr, check_idx)."""
+    rng = np.random.default_rng(seed)
+    m = n * dv // dc
+    while True:
+        sockets = np.repeat(np.arange(n), dv)
+        rng.shuffle(sockets)
+        rows = sockets.reshape(m, dc)
+        srt = np.sort(rows, axis=1)
+        bad = (np.diff(srt, axis=1) == 0).any(axis=1)
+        if not bad.any():
+            break
+        # repair: re-shuffle only the rows with a repeated bit (rare)
+        for _ in range(100):
+            idx = np.nonzero(bad)[0]
+            if idx.size == 0:
+                break
+            pool = np.concatenate([rows[idx].ravel(), rows[rng.integers(0, m, idx.size)].ravel()])
+            rng.shuffle(pool)
+            rows[idx] = pool[: idx.size * dc].reshape(idx.size, dc)
+            srt = np.sort(rows, axis=1)
+            bad = (np.diff(srt, axis=1) == 0).any(axis=1)
+        if not bad.any() and np.bincount(rows.ravel(), minlength=n).max() == dv:
+            break
+    rows = np.sort(rows, axis=1)
+    return m, np.arange(0, m * dc + 1, dc, dtype=np.int32), rows.ravel().astype(np.int32)
+
+
+@pytest.fixture(scope="module")
+def big():
+    n = 40000
+    m, cp, ci = regular_code(n, seed=11)
+    return n, m, cp, ci
+
+
+def test_large_code_parses_and_validates(big):
+    """CPU side: creation reaches the device step (no size limit below the plan's)."""
+    import ctypes as C
+    from qkd_ldpc_amd import _native as N
+    n, m, cp, ci = big
+    st = C.c_int(-1)
+    h = N.lib().qkd_code_create(n, m, cp.ctypes.data, ci.ctypes.data, 0, C.byref(st))
+    if h:
+        N.lib().qkd_code_destroy(h)
+    assert st.value == (N.ERR_DEVICE if N.lib().qkd_device_count() == 0 else N.OK), N.last_error()
+
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def Q():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import qkd_ldpc_amd as Q
+    return Q
+
+
+@pytest.fixture(scope="module")
+def big_codes(big, Q, oracle_mod, tmp_path_factory):
+    n, m, cp, ci = big
+    H = Q.HMatrix.from_check_lists(n, cp, ci)
+    cptr, cidx, bptr, bidx = H.adjacency()
+    p = str(tmp_path_factory.mktemp("big") / "big.alist")
+    write_alist(p, n, m, bptr, bidx, cptr, cidx)
+    return H, oracle_mod.Code.from_alist(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,thr,thr_on", [(0.03, 100.0, True), (0.06, 2.5, True), (0.04, 0.0, False)])
+def test_large_code_decode_bit_exact(Q, big_codes, oracle_mod, q, thr, thr_on):
+    H, oc = big_codes
+    n = H.num_bit_nodes
+    frames = []
+    for s in oracle_mod.seeds(99, 6):
+        a, b, qq = oracle_mod.keygen(int(s), n, q)
+        lp = np.log((1 - qq) / qq)
+        frames.append((np.where(b == 1, -lp, lp), oc.syndrome(a)))
+    llr = np.stack([f[0] for f in frames])
+    syn = np.stack([f[1] for f in frames]).astype(np.uint8)
+    r = Q.sum_product_decoding(H, torch.from_numpy(llr).cuda(), torch.from_numpy(syn).cuda(), 40,
+                               thr if thr_on else 100.0, thr_on)
+    torch.cuda.synchronize()
+    for f in range(len(frames)):
+        want = oc.decode(llr[f], syn[f], 40, thr, thr_on)
+        assert int(r.iterations[f]) == want["iters"]
+        assert bool(r.syndromes_match[f]) == want["sp_ok"]
+        assert (r.bits[f].cpu().numpy() == want["out"]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [0.03, 0.11])
+def test_large_code_trials_equal_oracle(Q, big_codes, oracle_mod, q):
+    """Fused trials (keygen + decode + compare); at q = 0.11 floor(N q) = 4400
+    flips take the serial key generator."""
+    H, oc = big_codes
+    seeds = oracle_mod.seeds(777, 8)
+    r = Q.run_trials(H, torch.from_numpy(seeds.view(np.int64)).cuda(), q, 0, 40)
+    torch.cuda.synchronize()
+    want = oc.trials(q, seeds, 0, 40, 100.0, True)
+    assert (r.iterations.cpu().numpy() == want["iters"]).all()
+    assert (r.syndromes_match.cpu().numpy().astype(bool) == want["sp_ok"]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == want["key_ok"]).all()
+    assert (r.exact_qber.cpu().numpy() == want["exact_q"]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["sp_f32", "minsum"])
+def test_large_code_variants_decode(Q, big_codes, variant):
+    H, _ = big_codes
+    seeds = torch.from_numpy(Q.make_seeds(5, 64).view(np.int64)).cuda()
+    r = Q.run_trials(H, seeds, 0.02, 0, 40, variant=variant)
+    torch.cuda.synchronize()
+    assert r.syndromes_match.cpu().numpy().all() and r.keys_match.cpu().numpy().all()

@@ -1,0 +1,39 @@
+"""Throughput of the large-code path (totals in global memory): a random
+(3,6)-regular code of N bits, F frames of fused trials at one QBER."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import qkd_ldpc_amd as Q  # noqa: E402
+from test_large_codes import regular_code  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=40000)
+ap.add_argument("--frames", type=int, default=4096)
+ap.add_argument("--qber", type=float, default=0.03)
+ap.add_argument("--variant", default="sp_f64")
+args = ap.parse_args()
+m, cp, ci = regular_code(args.n, seed=11)
+H = Q.HMatrix.from_check_lists(args.n, cp, ci)
+seeds = torch.from_numpy(Q.make_seeds(777, args.frames).view(np.int64)).cuda()
+a, b, q = Q.keygen(H, seeds, args.qber)
+Q.qkd_ldpc(H, a, b, float(q[0]), 50, variant=args.variant)
+torch.cuda.synchronize()
+t = time.perf_counter()
+steps = 5
+for _ in range(steps):
+    r = Q.qkd_ldpc(H, a, b, float(q[0]), 50, variant=args.variant)
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t) / steps
+it = r.iterations.cpu().numpy()
+print(json.dumps({"n": args.n, "m": m, "frames": args.frames, "qber": args.qber, "variant": args.variant,
+                  "ms_per_batch": dt * 1e3, "gbit_s": args.frames * args.n / dt / 1e9,
+                  "mean_it": float(it.mean()), "fer": float(1 - r.keys_match.cpu().numpy().mean())}))
