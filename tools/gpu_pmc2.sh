@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-variants"}
 k=0
 while read -r grp; do
   [ -z "$grp" ] && continue

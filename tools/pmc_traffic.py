@@ -11,10 +11,13 @@ import os
 import sys
 
 
+KERNEL = os.environ.get("QKD_PMC_KERNEL", "decode_kernel<1, 0,")   # binary64 keys path
+
+
 def per_launch(d, counter):
     vals = []
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        if "decode_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
             vals.append(float(r["Counter_Value"]))
     return sum(vals) / len(vals), len(vals)
 
@@ -23,7 +26,7 @@ def main():
     fetch_kb, nf = per_launch(sys.argv[1], "FETCH_SIZE")
     write_kb, nw = per_launch(sys.argv[2], "WRITE_SIZE")
     out = {
-        "kernel": "qkd::decode_kernel<1,6,true> (qkd_qkd_ldpc_batch, 4096 frames, QBER 0.02)",
+        "kernel": KERNEL + " (qkd_qkd_ldpc_batch, 4096 frames, QBER 0.02)",
         "fetch_size_kb": fetch_kb,
         "write_size_kb": write_kb,
         "launches": [nf, nw],
