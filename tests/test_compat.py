@@ -159,3 +159,32 @@ def test_compat_too_small_qber_throws_reference_message(driver):
     p = subprocess.run([driver], input="\n".join(lines + ["cfg 10 100.0 1 1 1", "trial 0.01 5"]) + "\n",
                        text=True, capture_output=True, timeout=120)
     assert "exception Key size '6' is too small for QBER." in p.stdout
+
+
+@pytest.mark.gpu
+def test_compat_variant_env_selects_minsum(driver, golden_code, oracle_mod):
+    """QKD_AMD_VARIANT=minsum runs the reference harness on the min-sum variant:
+    its batch point equals the library's own min-sum trials; an unknown name
+    throws like the reference's errors do."""
+    import qkd_ldpc_amd as Q
+    import torch
+    g = golden_code
+    lines = _code_cmd(10240, 5231, g["chk_off"], g["chk_idx"]) + ["cfg 50 100.0 1 512 777", "batch 1 0.06"]
+    env = dict(os.environ, QKD_AMD_VARIANT="minsum")
+    p = subprocess.run([driver], input="\n".join(lines) + "\n", text=True, capture_output=True,
+                       timeout=600, env=env)
+    assert p.returncode == 0, p.stderr
+    v = [ln for ln in p.stdout.splitlines() if ln.startswith("point")][0].split()
+    H = Q.HMatrix.from_check_lists(10240, g["chk_off"], g["chk_idx"])
+    seeds = torch.from_numpy(Q.make_seeds(777, 512).view(np.int64)).cuda()
+    r = Q.run_trials(H, seeds, 0.06, 0, 50, variant="minsum")
+    torch.cuda.synchronize()
+    it = r.iterations.cpu().numpy()
+    sp = r.syndromes_match.cpu().numpy().astype(bool)
+    st = oracle_mod.batch_stats(it, sp, r.keys_match.cpu().numpy(), r.exact_qber.cpu().numpy(), 512, 50)
+    assert float(v[3]) == st["iterations_successful_sp_mean"]
+    assert float(v[8]) == st["ratio_trials_successful_ldpc"]
+    env["QKD_AMD_VARIANT"] = "bogus"
+    p = subprocess.run([driver], input="\n".join(lines) + "\n", text=True, capture_output=True,
+                       timeout=600, env=env)
+    assert "unknown decoder variant 'bogus'" in p.stdout + p.stderr
