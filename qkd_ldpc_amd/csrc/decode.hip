@@ -197,6 +197,9 @@ struct DecodeLds {
 // (bits tid + r*kDecodeBlock) per load batch.
 constexpr int kDvUnroll = 3;
 constexpr int kBitChunk = 5;
+// the second-iteration table index and the first-message fold read a bit's
+// messages from the unrolled rows only
+static_assert(kTab2MaxDv <= kDvUnroll, "tables need every row of their bits unrolled");
 // Plan-walking loops outside the check phase load this many tasks' plan words
 // per trip (the plan carries kPlanPadTasks >= kPlanGroup * NW idle tasks).
 constexpr int kPlanGroup = 4;

@@ -17,7 +17,7 @@ constexpr int kDecodeBlock = 1024;
 // Second-iteration tanh table (decode.hip): entries per degree pattern are
 // 2^(1 + max_dv) sign codes x max_dv rows; the table is used when
 // max_dv <= kTab2MaxDv and n_pat * entries <= kTab2MaxEntries.
-constexpr int kTab2MaxDv = 4;
+constexpr int kTab2MaxDv = 3;   // <= the bit phase's unrolled rows (decode.hip kDvUnroll)
 constexpr int kTab2MaxEntries = 2048;
 __host__ __device__ inline int tab2_stride(int max_dv) { return (1 << (1 + max_dv)) * max_dv; }
 

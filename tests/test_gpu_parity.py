@@ -352,3 +352,34 @@ def test_keygen_kernels_agree_with_oracle(Q, oracle_mod, monkeypatch, mode):
             wa, wb, wq = oracle_mod.keygen(int(s), n, q)
             assert (a[f] == wa).all() and (b[f] == wb).all(), (mode, n, q, f)
             assert qq[f] == wq
+
+
+def test_irregular_high_degree_bits_keys_path(Q, oracle_mod, tmp_path):
+    """Bit degrees 2..6 (beyond the unrolled rows and the table limit): the fused
+    trial path takes the general first/second iterations and the bit phase's
+    tail rows; results equal the oracle."""
+    from conftest import write_alist
+    rng = np.random.default_rng(21)
+    n, m = 3000, 1500
+    degs = rng.choice([2, 3, 4, 5, 6], size=n, p=[0.2, 0.4, 0.2, 0.1, 0.1])
+    rows = [[] for _ in range(m)]
+    for i in range(n):
+        for j in rng.choice(m, size=degs[i], replace=False):
+            rows[j].append(i)
+    rows = [sorted(r) for r in rows if r] 
+    m = len(rows)
+    co = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int32)
+    ci = np.concatenate(rows).astype(np.int32)
+    H = Q.HMatrix.from_check_lists(n, co, ci)
+    cptr, cidx, bptr, bidx = H.adjacency()
+    p = str(tmp_path / "irr.alist")
+    write_alist(p, n, m, bptr, bidx, cptr, cidx, pad=False)
+    oc = oracle_mod.Code.from_alist(p)
+    seeds = oracle_mod.seeds(31, 24)
+    for q in (0.02, 0.06):
+        r = Q.run_trials(H, seeds_dev(seeds), q, 0, 30)
+        torch.cuda.synchronize()
+        want = oc.trials(q, seeds, 0, 30, 100.0, True)
+        assert (r.iterations.cpu().numpy() == want["iters"]).all()
+        assert (r.syndromes_match.cpu().numpy().astype(bool) == want["sp_ok"]).all()
+        assert (r.keys_match.cpu().numpy().astype(bool) == want["key_ok"]).all()
