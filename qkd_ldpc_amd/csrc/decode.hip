@@ -250,6 +250,13 @@ template <> struct RuleMath<kRuleSp32> {
     }
 };
 
+// A check-phase message store. (Non-temporal stores, which skip L2, measured
+// 2x slower: the bit phase re-reads these lines shortly after.)
+template <typename T>
+__device__ __forceinline__ void msg_store(T* p, T v) {
+    *p = v;
+}
+
 // Makes this wave's LDS row writes visible to its own lanes (no s_barrier).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -383,7 +390,7 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
     T* pend = nullptr;      // message computed by the previous task, not yet stored
     T pv = 0;
     for (;;) {
-        if (pend) *pend = pv;
+        if (pend) msg_store(pend, pv);
         const uint2 wc = pl[(t + 2 * NW) * 64];
         const T xb = src(wb);
         const T ob = FIRST ? (T)0 : *msg(wb);
@@ -391,7 +398,7 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
         pend = msg(wa);
         t += NW;
         if (t >= n_tasks) break;
-        *pend = pv;
+        msg_store(pend, pv);
         wa = pl[(t + 2 * NW) * 64];
         xa = src(wc);
         oa = FIRST ? (T)0 : *msg(wc);
@@ -1368,6 +1375,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     qkd_status s = decode_grid(c, fn, lds, &grid);
     if (s != QKD_OK) return s;
     grid = (int)std::min<size_t>((size_t)grid, a.n_frames);
+    // diagnostic: QKD_DECODE_GRID caps the resident workgroups (frames in flight)
+    if (const char* g = getenv("QKD_DECODE_GRID")) grid = std::max(1, std::min(grid, atoi(g)));
     s = ws_reserve_decode(ws, rule == kRuleMinSumLds ? 0 : (size_t)grid);   // no global messages
     if (s != QKD_OK) return s;
     a.code = c->view();
