@@ -34,6 +34,7 @@
 #include "qkd_math.h"
 #include "qkd_plan.h"
 #include "qkd_rng.h"
+#include "qkd_decode.h"
 
 // Diagnostic builds only (tools/exp_run.sh; never the shipped library): the
 // QKD_EXP_NO_STOP / QKD_EXP_NO_MATH / QKD_EXP_MSG_LOCAL / QKD_EXP_MSG_SMALL
@@ -44,290 +45,6 @@
 // builds are wrong by design.
 
 namespace qkd {
-
-// Largest check degree the first-iteration table covers.
-constexpr int kFirstTableDeg = 16;
-
-
-enum DecodeMode : int {
-    kModeLlr = 0,  // qkd_decode_batch: caller LLRs + syndrome bytes
-    kModeKeys = 1  // QKD_LDPC path: packed alice/bob keys, LLR = +-log_p
-};
-
-// Check-node rule and message width (QKD_VARIANT_* in qkd_ldpc.h).
-//   kRuleSp64   the reference's sum-product in binary64, bit-exact
-//   kRuleSp32   the same schedule with binary32 messages and totals, OCML
-//               tanhf/atanhf (a variant: not bit-exact to anything)
-//   kRuleMinSum normalised min-sum in binary32: c2b = scale * sign * min|b2c|
-//               over the other edges of the check (a variant, no transcendental)
-//   kRuleMinSumLds  the same min-sum with the frame's whole message state in
-//               LDS (per check: min1, min2, argmin, sign bits), no global
-//               message store; used when the state fits (decode_ms_fits)
-enum DecodeRule : int { kRuleSp64 = 0, kRuleSp32 = 1, kRuleMinSum = 2, kRuleMinSumLds = 3 };
-template <int RULE> struct RuleMsg { using T = float; };
-template <> struct RuleMsg<kRuleSp64> { using T = double; };
-
-struct DecodeArgs {
-    DeviceCode code;
-    uint32_t n_frames;
-    uint32_t max_it;
-    double thr;
-    int clamp_on;
-    float ms_scale;    // kRuleMinSum normalisation
-    // kModeLlr
-    const double* llr;
-    const uint8_t* syn;
-    // kModeKeys
-    const uint64_t* alice_w;
-    const uint64_t* bob_w;
-    uint32_t words;
-    double log_p;
-    // First-iteration message table (kModeKeys): with every channel LLR equal
-    // to +-log_p, the first check phase is a function of signs and degrees
-    // only (see first_check_phase); first_c2b[d] = its message magnitude for
-    // a check of degree d. Used when first_table != 0.
-    int first_table;
-    double first_c2b[kFirstTableDeg + 1];
-    // Second-iteration tanh table (kModeKeys, needs first_table): entries,
-    // 0 when off (see second_table_fill).
-    int tab2_entries;
-    // outputs
-    uint8_t* bits_out;
-    uint32_t* iters;
-    uint8_t* sp_ok;
-    uint8_t* key_ok;
-    // scratch
-    double* c2b;
-    size_t c2b_stride;
-    uint32_t* counter;
-    // diagnostics: per-phase shader-clock cycles summed over workgroups
-    // (thread 0's view between barriers), or nullptr
-    unsigned long long* phase;
-    // qkd_trace_decode (binary64 rule, one frame): per executed iteration, the
-    // c2b store (max_dv x n_pad) then the bit totals (n_pad), or nullptr
-    double* trace;
-    size_t trace_stride;
-    // large codes (decode_kernel<..., GT = true>): the bit totals of each
-    // workgroup's frame in global scratch, totals_stride doubles apart
-    double* totals;
-    size_t totals_stride;
-};
-
-// Phase-clock accumulation (diagnostic; a wave-uniform test when off). Each
-// mark adds straight to the global slot, so nothing is indexed dynamically in
-// registers (an accumulator array would live in scratch).
-struct PhaseClock {
-    unsigned long long* out;
-    long long t = 0;
-    __device__ explicit PhaseClock(unsigned long long* o) : out(threadIdx.x == 0 ? o : nullptr) {
-        if (out) t = clock64();
-    }
-    __device__ __forceinline__ void mark(int k) {
-        if (out) {
-            const long long n = clock64();
-            atomicAdd(out + k, (unsigned long long)(n - t));
-            t = n;
-        }
-    }
-    __device__ void flush() {}
-};
-
-template <typename T>
-__device__ __forceinline__ T clamp_msg(T v, T thr) {
-    // threshold_matrix_irregular (array_and_matrix_operations.cpp:508-524):
-    // compare-based, so NaN passes through.
-    return v > thr ? thr : (v < -thr ? -thr : v);
-}
-
-// Block-wide any(); flags[2] live in LDS and alternate between calls. Every
-// call must be separated from the next by at least one __syncthreads().
-__device__ __forceinline__ bool block_any(bool p, uint32_t* flags, uint32_t& k) {
-    uint32_t* f = flags + (k & 1u);
-    const bool wave_hit = __any(p);
-    if (wave_hit && (threadIdx.x & 63) == 0) atomicOr(f, 1u);
-    __syncthreads();
-    const bool r = *f != 0;
-    if (threadIdx.x == 0) flags[(k + 1) & 1u] = 0;
-    k++;
-    return r;
-}
-
-
-// Syndrome bit arrays hold whole 64-check groups (written by one ballot each).
-__host__ __device__ inline int decode_m_words(int m) { return ((m + 63) / 64) * 2; }
-
-// LDS layout of decode_kernel (bytes):
-//   total  [n_pad]          bit totals (the reference's `total`, :256-267), message width
-//   tsyn   [m_words]        target syndrome, one bit per check
-//   xsyn   [m_words]        syndrome of the current hard decision (XOR-built)
-//   qsyn   [m_words]        QKD path: sign of each check's first-iteration product
-//   tval   [NW][64 + DC]    per-wave tanh values for the in-check products
-//                           (prologue: the frame's Alice + Bob words)
-//   ctab   [kFirstTableDeg+1] first-iteration message magnitudes by degree
-//   tab2   [tab2_entries]   second-iteration tanh table
-//   t2idx  [n_pad]          per-bit base index into tab2 (uint16)
-//   ctl    [4]              frame index, block_any flags
-//   cst    [m] (uint4)      kRuleMinSumLds: per-check min-sum state (ms_state)
-struct DecodeLds {
-    size_t tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, cst, bytes;
-    // total_esz: bytes per bit total in LDS (0: the totals live in global
-    // memory, large codes)
-    __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries, int total_esz,
-                                  int cst_checks = 0, int row_esz = 0) {
-        const int m_words = decode_m_words(m);
-        const int esz = row_esz ? row_esz : total_esz;
-        tsyn = ((size_t)n_pad * total_esz + 15) & ~(size_t)15;
-        xsyn = tsyn + (size_t)m_words * 4;
-        qsyn = xsyn + (size_t)m_words * 4;
-        tval = (qsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
-        // the tanh rows double as the prologue's staging area for the frame's
-        // Alice and Bob words
-        const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * esz;
-        const size_t stage = (size_t)n_words * 16;
-        ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
-        tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
-        t2idx = tab2 + (size_t)tab2_entries * 8;
-        ctl = (t2idx + (tab2_entries ? (size_t)n_pad * 2 : 0) + 15) & ~(size_t)15;
-        cst = ctl + 16;
-        bytes = cst + (size_t)cst_checks * 16;
-    }
-};
-
-// Bit phase: message rows per bit loaded ahead of the ordered sum, and rounds
-// (bits tid + r*kDecodeBlock) per load batch.
-constexpr int kDvUnroll = 3;
-constexpr int kBitChunk = 5;
-// the second-iteration table index and the first-message fold read a bit's
-// messages from the unrolled rows only
-static_assert(kTab2MaxDv <= kDvUnroll, "tables need every row of their bits unrolled");
-// Plan-walking loops outside the check phase load this many tasks' plan words
-// per trip (the plan carries kPlanPadTasks >= kPlanGroup * NW idle tasks).
-constexpr int kPlanGroup = 4;
-
-// ---- wave-plan words (qkd_plan.h) ------------------------------------------
-__device__ __forceinline__ uint32_t pw_bit(uint2 p) { return p.x & qkdp::kPlanBitMask; }
-__device__ __forceinline__ uint32_t pw_row(uint2 p) { return p.x >> 24; }
-__device__ __forceinline__ uint32_t pw_chk(uint2 p) { return p.y & qkdp::kPlanChkMask; }
-__device__ __forceinline__ int pw_start(uint2 p) { return (int)((p.y >> 20) & 63u); }
-__device__ __forceinline__ int pw_deg(uint2 p) { return (int)(p.y >> 26) + 1; }
-// Parity of the lanes of this lane's check (its segment) in a wave ballot.
-__device__ __forceinline__ int seg_parity(uint64_t ballot, uint2 w) {
-    const int deg = pw_deg(w);
-    const uint64_t m = deg == 64 ? ~0ull : ((1ull << deg) - 1ull);
-    return __popcll(ballot & (m << pw_start(w))) & 1;
-}
-
-// One edge of the check phase (qkd_ldpc_algorithm.cpp:220-249):
-//   b2c = FIRST ? LLR_i : clamp(total_i - c2b)                  (:188, :303-316)
-//   t   = tanh(b2c / 2)                                         (:224)
-//   P   = (s_j ? -1 : 1) * t_0 * t_1 * ...  (ascending bits)    (:231-235)
-//   c2b = clamp(2 * atanh(P / t))                               (:239-249)
-// `row` is this wave's LDS row of tanh values (64 + DC doubles, so reads past
-// a segment's end stay inside it and are discarded).
-// Where a check phase takes its incoming tanh values from.
-enum CheckSrc : int {
-    kSrcGeneral = 0,   // tanh(clamp(total_i - c2b) / 2)
-    kSrcFirst = 1,     // first iteration: tanh(LLR_i / 2)
-    kSrcTable = 2      // second QKD iteration: looked up (second_table_index)
-};
-
-template <int RULE> struct RuleMath;
-template <> struct RuleMath<kRuleSp64> {
-    static __device__ __forceinline__ double tanh_half(double x) { return qkdm::tanh_flat(x / 2.0); }
-    static __device__ __forceinline__ double two_atanh(double p) { return 2.0 * qkdm::atanh_flat(p); }
-};
-template <> struct RuleMath<kRuleSp32> {
-    static __device__ __forceinline__ float tanh_half(float x) { return tanhf(x * 0.5f); }
-    // In binary32, tanh(b2c / 2) rounds to 1 from |b2c| ~ 18 on, so the
-    // extrinsic ratio P / t lands on (or one ulp beyond) +-1 far more often
-    // than in binary64, and 2 atanh(+-1) = +-inf would turn a ~17 message into
-    // the clamp value. The ratio is therefore limited to the largest binary32
-    // below 1 (|message| <= 2 atanh(1 - 2^-24) = 17.33); NaN (0/0) still passes.
-    static __device__ __forceinline__ float two_atanh(float p) {
-        constexpr float kMax = 0x1.fffffep-1f;
-        p = p > kMax ? kMax : (p < -kMax ? -kMax : p);
-        return 2.0f * atanhf(p);
-    }
-};
-
-// A check-phase message store. (Non-temporal stores, which skip L2, measured
-// 2x slower: the bit phase re-reads these lines shortly after.)
-template <typename T>
-__device__ __forceinline__ void msg_store(T* p, T v) {
-    *p = v;
-}
-
-// Makes this wave's LDS row writes visible to its own lanes (no s_barrier).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// First half of an edge: the value the lane publishes in its wave's LDS row.
-//   sum-product: t = tanh(b2c / 2) (or the tabulated t), min-sum: b2c itself.
-template <int SRC, bool CLAMP, int RULE, typename T>
-__device__ __forceinline__ T edge_in(T x, T old, T thr) {
-    if (SRC == kSrcGeneral) {
-        x = x - old;
-        if (CLAMP) x = clamp_msg(x, thr);
-    }
-#ifdef QKD_EXP_NO_MATH
-    return x * (T)0.5;
-#endif
-    if constexpr (RULE == kRuleMinSum) return x;
-    else return SRC == kSrcTable ? x : RuleMath<RULE>::tanh_half(x);
-}
-
-// Second half: the lane's message from the published row of its check
-// (segment [start, start + deg) of `row`; the row has 64 + DC entries, so reads
-// past a segment's end stay inside it and are discarded).
-template <bool CLAMP, int DC, int RULE, typename T>
-__device__ __forceinline__ T edge_out(T tv, uint2 w, uint32_t sbit, int lane, T thr, const T* row,
-                                      float ms_scale) {
-    const int start = pw_start(w);
-    const int deg = pw_deg(w);
-    T o[DC];
-#pragma unroll
-    for (int k = 0; k < DC; ++k) o[k] = row[start + k];
-    T v;
-    if constexpr (RULE == kRuleMinSum) {
-        // c2b = scale * (s_j ^ signs of the other b2c) * min over the other |b2c|
-        uint32_t neg = sbit ^ (tv < 0 ? 1u : 0u);
-        T mn = __builtin_inff();
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            if (k < deg) {
-                neg ^= o[k] < 0 ? 1u : 0u;
-                if (start + k != lane) mn = fminf(mn, fabsf(o[k]));
-            }
-        }
-        v = (T)ms_scale * mn;
-        v = neg ? -v : v;
-    } else if constexpr (RULE == kRuleSp64) {
-        // the reference's P = (s_j ? -1 : 1) * prod_k t_k, then 2 atanh(P / t_self) (:231-241)
-        T P = sbit ? (T)-1 : (T)1;
-        P = P * o[0];                         // every check has degree >= 1
-#pragma unroll
-        for (int k = 1; k < DC; ++k) P = k < deg ? P * o[k] : P;
-#ifdef QKD_EXP_NO_MATH
-        v = P + tv;
-#else
-        v = RuleMath<RULE>::two_atanh(P / tv);
-#endif
-    } else {
-        // binary32 variant: the extrinsic product over the other edges in
-        // ascending order, no division. (P / t is 0/0 = NaN when b2c is
-        // exactly 0, which binary32 cancellation makes a ~1 % per-frame
-        // event at QBER 0.05, and the NaN then floods the frame.)
-        T P = sbit ? (T)-1 : (T)1;
-#pragma unroll
-        for (int k = 0; k < DC; ++k) P = (k < deg && start + k != lane) ? P * o[k] : P;
-        v = RuleMath<RULE>::two_atanh(P);
-    }
-    if (CLAMP) v = clamp_msg(v, thr);
-    return v;
-}
 
 // The check phase of one iteration for one wave: tasks wave, wave + NW, ...
 // Per edge (qkd_ldpc_algorithm.cpp:220-249):
@@ -497,48 +214,6 @@ __device__ __forceinline__ void ms_check_phase(const DeviceCode& c, const uint32
     }
 }
 
-// Second check phase of the QKD path. After the first iteration every message
-// is +-C_d (first_check_phase), so bit i's total is
-//   total_i = ((LLR_i + c_0) + c_1) + ...    c_k = sign_k * C_{d_k}   (:256-267)
-// and its second-iteration incoming value for its k-th check is
-//   t = tanh(clamp(total_i - c_k) / 2)                            (:303-316, :224)
-// a function of (the degrees d_k of bit i's checks, bob_i, sign_0.., k). The
-// table holds it for every degree pattern p, sign code and row k:
-//   tab2[p * stride + code * max_dv + k],  code = bob_i | sign_k << (1 + k)
-// computed with the same binary64 operations in the same order. The
-// iteration-1 bit phase records each bit's base index (second_table_index).
-template <bool CLAMP>
-__device__ void second_table_fill(const DeviceCode& c, const double* ctab, double log_p, double thr,
-                                  double* tab2, int entries) {
-    const int dvm = c.max_dv;
-    const int stride = tab2_stride(dvm);
-    for (int e = threadIdx.x; e < entries; e += kDecodeBlock) {
-        const int p = e / stride;
-        const int r = e - p * stride;
-        const int code = r / dvm;
-        const int k = r - code * dvm;
-        const uint8_t* degs = c.pat_deg + p * dvm;
-        double total = (code & 1) ? -log_p : log_p;
-        double ck = 0.0;
-        int dv = 0;
-        for (int m = 0; m < dvm; ++m) {
-            if (degs[m] == 0) break;
-            const double cm = ctab[degs[m]];
-            const double v = ((code >> (1 + m)) & 1) ? -cm : cm;
-            total = total + v;
-            if (m == k) ck = v;
-            dv = m + 1;
-        }
-        double y = 0.0;
-        if (k < dv) {
-            double b = total - ck;
-            if (CLAMP) b = clamp_msg(b, thr);
-            y = qkdm::tanh_flat(b / 2.0);
-        }
-        tab2[e] = y;
-    }
-    __syncthreads();
-}
 
 // fold_first_message: when the second table is also in use, nothing reads the
 // first iteration's stored messages (the second check phase takes its inputs
@@ -1180,7 +855,6 @@ __global__ void counters_init_kernel(qkd_counters* c) {
 
 // ---- launch plumbing --------------------------------------------------------
 
-using DecodeFn = void (*)(DecodeArgs);
 
 // Check-degree buckets: the in-check product reads DC values per lane.
 template <int MODE, int RULE, bool CLAMP, bool GT>
@@ -1364,6 +1038,46 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     const bool ms_global = ms_store && !strcmp(ms_store, "global");
     if (rule == kRuleMinSum && !ms_global && decode_ms_fits(c)) rule = kRuleMinSumLds;
     a.ms_scale = minsum_scale_of(flags);
+    // The split-store kernel (decode_split.hip) for the sum-product rules
+    // whenever its LDS layout fits; QKD_DECODE_KERNEL=classic keeps
+    // decode_kernel (A/B measurements, tests). Trace mode records the classic
+    // kernel's store.
+    const char* kern = getenv("QKD_DECODE_KERNEL");
+    const bool classic = kern && !strcmp(kern, "classic");
+    if ((rule == kRuleSp64 || rule == kRuleSp32) && !classic && !a.trace && c->n <= kMaxBitsLds) {
+        int sdc = 0;
+        DecodeFn sfn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &sdc);
+        const int esz = rule == kRuleSp64 ? 8 : 4;
+        // diagnostic: QKD_SPLIT_BUDGET lowers the LDS budget (fewer LDS slots)
+        size_t budget = kLdsBytesMax;
+        if (const char* b = getenv("QKD_SPLIT_BUDGET")) budget = std::min(budget, (size_t)atol(b));
+        const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, esz, budget);
+        if (L.bytes <= kLdsBytesMax && L.S > (uint32_t)c->n) {
+            int grid = 0;
+            qkd_status s = decode_grid(c, sfn, L.bytes, &grid);
+            if (s != QKD_OK) return s;
+            grid = (int)std::min<size_t>((size_t)grid, a.n_frames);
+            if (const char* g = getenv("QKD_DECODE_GRID")) grid = std::max(1, std::min(grid, atoi(g)));
+            s = ws_reserve_decode(ws, (size_t)grid);
+            if (s != QKD_OK) return s;
+            a.code = c->view();
+            a.c2b = ws->c2b;
+            const size_t slots = (size_t)c->max_dv * c->n_pad;
+            a.c2b_stride = (slots - L.S + 31) & ~(size_t)31;      // elements of the message type
+            a.lds_budget = (uint32_t)budget;
+            a.counter = ws->counter;
+            QKD_HIP(hipMemsetAsync(ws->counter, 0, 4, stream));
+            static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;
+            a.phase = nullptr;
+            if (timing) {
+                a.phase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 64);
+                QKD_HIP(hipMemsetAsync(a.phase, 0, 64, stream));
+            }
+            hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
+            QKD_HIP(hipGetLastError());
+            return QKD_OK;
+        }
+    }
     const bool gt = decode_needs_gt(c, rule, a.tab2_entries);
     if (gt) {                                     // large code: no per-bit LDS tables
         a.first_table = 0;

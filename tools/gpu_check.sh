@@ -19,7 +19,7 @@ step() {  # name timeout cmd...
 STEPS=${STEPS:-"tests smoke bench prof"}
 for s in $STEPS; do
   case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
