@@ -207,6 +207,14 @@ QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t 
  * reference counterpart (the reference prints TRACE_* arrays instead,
  * qkd_ldpc_algorithm.cpp:42-155). */
 QKD_API qkd_status qkd_debug_phase_cycles(qkd_workspace *ws, uint64_t *cycles7);
+/* Frames of the QKD path (qkd_qkd_ldpc_batch / qkd_trials_batch, binary64
+ * rule, clamp on) whose speculative interval iterations could not certify a
+ * hard decision (or reached the cap) and were decoded again with the exact
+ * iterations, accumulated over the launches on `ws` since the last reset;
+ * reset != 0 zeroes the count. QKD_SPEC_CAP=<k> in the environment sets how
+ * many interval iterations a frame may run first (0: off; default 8).
+ * Outputs never depend on it. No reference counterpart. */
+QKD_API qkd_status qkd_debug_spec_replays(qkd_workspace *ws, uint64_t *replays, int reset);
 /* Trace of one frame, the reference's TRACE_SUM_PRODUCT / TRACE_SUM_PRODUCT_LLR
  * (qkd_ldpc_algorithm.cpp:212-330): decodes llr[N] / syndrome[M] (host arrays)
  * with the reference rule (QKD_VARIANT_SP_F64 only) and records, for every
@@ -225,7 +233,9 @@ QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, con
  * x[n] -> y[n] (device arrays): the bit-exactness check of the device build
  * against glibc (reference qkd_ldpc_algorithm.cpp:224, :241). which = 2 / 3:
  * the binary32 variant's tanh(x/2) / 2*atanh(x) (QKD_VARIANT_SP_F32), x
- * rounded to binary32, result widened. */
+ * rounded to binary32, result widened. which = 4 / 5: certified bounds of
+ * phi(x) = -ln tanh(x/2) over [x[2k], x[2k+1]] (the speculative iterations'
+ * input / output forms, qkd_spec.h) -> y[2k] = lower, y[2k+1] = upper; n even. */
 QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
 
 /* ---- host helpers --------------------------------------------------------- */

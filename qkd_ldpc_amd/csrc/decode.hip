@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <limits>
 #include <cstdlib>
 #include <cstring>
 
@@ -35,6 +37,7 @@
 #include "qkd_plan.h"
 #include "qkd_rng.h"
 #include "qkd_decode.h"
+#include "qkd_spec.h"
 
 // Diagnostic builds only (tools/exp_run.sh; never the shipped library): the
 // QKD_EXP_NO_STOP / QKD_EXP_NO_MATH / QKD_EXP_MSG_LOCAL / QKD_EXP_MSG_SMALL
@@ -951,7 +954,10 @@ static qkd_status decode_grid(const qkd_code* c, DecodeFn fn, size_t lds, int* g
 
 qkd_status ws_reserve_decode(qkd_workspace* ws, size_t slots) {
     const qkd_code* c = ws->code;
-    if (!ws->counter) QKD_HIP(hipMalloc(&ws->counter, 128));
+    if (!ws->counter) {
+        QKD_HIP(hipMalloc(&ws->counter, 128));
+        QKD_HIP(hipMemset(ws->counter, 0, 128));
+    }
     if (ws->c2b_slots >= slots) return QKD_OK;
     if (ws->c2b) QKD_HIP(hipFree(ws->c2b));
     ws->c2b = nullptr;
@@ -971,10 +977,18 @@ qkd_status ws_reserve_keys(qkd_workspace* ws, size_t frames, size_t low_words) {
     if (ws->key_frames < frames) {
         if (ws->alice_w) QKD_HIP(hipFree(ws->alice_w));
         if (ws->bob_w) QKD_HIP(hipFree(ws->bob_w));
-        ws->alice_w = ws->bob_w = nullptr;
+        if (ws->synw) QKD_HIP(hipFree(ws->synw));
+        if (ws->zout) QKD_HIP(hipFree(ws->zout));
+        if (ws->replay) QKD_HIP(hipFree(ws->replay));
+        ws->alice_w = ws->bob_w = ws->zout = nullptr;
+        ws->synw = ws->replay = nullptr;
         ws->key_frames = 0;
+        const size_t syn_words = 2 * (size_t)decode_m_words(c->m);
         if (hipMalloc(&ws->alice_w, frames * words * 8) != hipSuccess ||
-            hipMalloc(&ws->bob_w, frames * words * 8) != hipSuccess)
+            hipMalloc(&ws->bob_w, frames * words * 8) != hipSuccess ||
+            hipMalloc(&ws->synw, frames * syn_words * 4) != hipSuccess ||
+            hipMalloc(&ws->zout, frames * words * 8) != hipSuccess ||
+            hipMalloc(&ws->replay, frames * 4) != hipSuccess)
             return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate keys for %zu frames", frames);
         ws->key_frames = frames;
     }
@@ -995,6 +1009,9 @@ static qkd_status ws_free(qkd_workspace* ws) {
     if (ws->counter) (void)hipFree(ws->counter);
     if (ws->alice_w) (void)hipFree(ws->alice_w);
     if (ws->bob_w) (void)hipFree(ws->bob_w);
+    if (ws->synw) (void)hipFree(ws->synw);
+    if (ws->zout) (void)hipFree(ws->zout);
+    if (ws->replay) (void)hipFree(ws->replay);
     if (ws->low) (void)hipFree(ws->low);
     if (ws->done) (void)hipEventDestroy(ws->done);
     return QKD_OK;
@@ -1066,15 +1083,42 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             a.c2b_stride = (slots - L.S + 31) & ~(size_t)31;      // elements of the message type
             a.lds_budget = (uint32_t)budget;
             a.counter = ws->counter;
-            QKD_HIP(hipMemsetAsync(ws->counter, 0, 4, stream));
+            // [0] frame queue of the first launch, [1] replay list length,
+            // [2] frame queue of the exact launch after a speculative one
+            QKD_HIP(hipMemsetAsync(ws->counter, 0, 12, stream));
             static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;
             a.phase = nullptr;
             if (timing) {
                 a.phase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 64);
                 QKD_HIP(hipMemsetAsync(a.phase, 0, 64, stream));
             }
+            a.replay_list = nullptr;
+            a.replay_count = ws->counter + 1;
+            if (mode == kModeKeys) {
+                a.synw = ws->synw;
+                a.zout = ws->zout;
+                a.spec_replays = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 120);
+                QKD_HIP(launch_frame_syn(a, stream));
+            }
+            // speculative interval iterations (qkd_spec.h) first, when they
+            // apply: QKD path with the folded first iteration, binary64 rule,
+            // clamped messages, bit degree <= kDvUnroll
+            const bool spec = mode == kModeKeys && rule == kRuleSp64 && a.spec_cap > 0 && a.clamp_on &&
+                              a.first_table && c->max_dv <= kDvUnroll && ws->replay;
+            if (spec) {
+                int xdc = 0, sgrid = 0;
+                DecodeFn xfn = pick_split_spec(c->max_dc, &xdc);
+                s = decode_grid(c, xfn, L.bytes, &sgrid);
+                if (s != QKD_OK) return s;
+                sgrid = std::min(sgrid, grid);
+                a.replay_list = ws->replay;
+                hipLaunchKernelGGL(xfn, dim3(sgrid), dim3(kDecodeBlock), L.bytes, stream, a);
+                QKD_HIP(hipGetLastError());
+                a.counter = ws->counter + 2;      // the exact launch takes the listed frames
+            }
             hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
             QKD_HIP(hipGetLastError());
+            if (mode == kModeKeys) QKD_HIP(launch_key_match(a, stream));
             return QKD_OK;
         }
     }
@@ -1201,6 +1245,14 @@ qkd_status qkd_decode_batch(const qkd_code* c, qkd_workspace* ws, const double* 
     return launch_decode(c, ws, a, kModeLlr, flags, (hipStream_t)stream);
 }
 
+// binary32 bound of a binary64 value: the largest float <= x (up: smallest >= x)
+static float f32_bound(double x, bool up) {
+    float f = (float)x;
+    if (up && (double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    if (!up && (double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+}
+
 // Shared by qkd_qkd_ldpc_batch and qkd_trials_batch: keys already packed in ws.
 static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_frames, double q,
                               uint32_t max_it, double thr, uint32_t flags, uint8_t* bits_out,
@@ -1228,6 +1280,16 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
         }
     }
     a.tab2_entries = (a.first_table && c->n_pat > 0) ? c->n_pat * tab2_stride(c->max_dv) : 0;
+    // speculative interval iterations (decode_split.hip, qkd_spec.h) ahead of
+    // the exact ones, for the binary64 rule with clamped messages;
+    // QKD_SPEC_CAP overrides how many (0: off)
+    int cap = kSpecCapDefault;
+    if (const char* e = getenv("QKD_SPEC_CAP")) cap = std::max(0, atoi(e));
+    a.spec_cap = (rule_of(flags) == kRuleSp64 && a.clamp_on && a.first_table) ? (uint32_t)cap : 0u;
+    a.lp_dn = f32_bound(a.log_p, false);
+    a.lp_up = f32_bound(a.log_p, true);
+    a.thr_dn = f32_bound(thr, false);
+    a.thr_up = f32_bound(thr, true);
     a.bits_out = bits_out;
     a.iters = iters;
     a.sp_ok = sp_ok;
@@ -1323,13 +1385,28 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
         case 0: y[i] = qkdm::tanh_flat(x[i]); break;
         case 1: y[i] = qkdm::atanh_flat(x[i]); break;
         case 2: y[i] = (double)RuleMath<kRuleSp32>::tanh_half((float)x[i]); break;
+        case 4:
+        case 5: {
+            // phi bounds over [x[2k], x[2k+1]] -> y[2k] = lo, y[2k+1] = hi
+            // (4: qkds::phi_bounds, 5: qkds::phi_bounds_out); one thread per pair
+            if (i & 1) break;
+            float lo, hi;
+            if (which == 4) qkds::phi_bounds((float)x[i], (float)x[i + 1], lo, hi);
+            else qkds::phi_bounds_out((float)x[i], (float)x[i + 1], lo, hi);
+            y[i] = lo;
+            y[i + 1] = hi;
+            break;
+        }
+        case 6: y[i] = (double)__builtin_amdgcn_exp2f((float)x[i]); break;   // hardware v_exp_f32
+        case 7: y[i] = (double)__builtin_amdgcn_logf((float)x[i]); break;    // hardware v_log_f32
         default: y[i] = (double)RuleMath<kRuleSp32>::two_atanh((float)x[i]); break;
     }
 }
 
 qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void* stream) {
     clear_error();
-    if (!x || !y || which < 0 || which > 3) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if (!x || !y || which < 0 || which > 7) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if ((which == 4 || which == 5) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "phi bounds take pairs (n even)");
     if (n == 0) return QKD_OK;
     hipLaunchKernelGGL(math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, which,
                        x, y, n);
@@ -1411,6 +1488,18 @@ qkd_status qkd_trace_decode(const qkd_code* c, const double* llr, const uint8_t*
     }
     cleanup();
     return s;
+}
+
+qkd_status qkd_debug_spec_replays(qkd_workspace* ws, uint64_t* replays, int reset) {
+    if (!ws || !replays) return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    *replays = 0;
+    if (!ws->counter) return QKD_OK;
+    DeviceGuard g(ws->device);
+    QKD_HIP(hipDeviceSynchronize());
+    char* p = reinterpret_cast<char*>(ws->counter) + 120;
+    QKD_HIP(hipMemcpy(replays, p, 8, hipMemcpyDeviceToHost));
+    if (reset) QKD_HIP(hipMemset(p, 0, 8));
+    return QKD_OK;
 }
 
 qkd_status qkd_debug_phase_cycles(qkd_workspace* ws, uint64_t* cycles7) {

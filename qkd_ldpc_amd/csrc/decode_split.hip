@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include "qkd_decode.h"
+#include "qkd_spec.h"
 
 namespace qkd {
 
@@ -159,10 +160,220 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
     ms.st(pend, pv);
 }
 
+// ---- speculative interval iterations (qkd_spec.h) ---------------------------
+// Check phase on intervals: each slot holds [lo, hi] of the edge's b2c on
+// entry and of its c2b on exit (two binary32 in the 8-byte slot). The
+// message's sign is exact (s_j and the signs of the other b2c, which the
+// intervals must certify); its magnitude is bounded in the phi domain
+// (qkd_spec.h). A b2c interval that does not exclude 0 (or is too
+// close to 0, or a sum too large, to certify) raises the abort bit of the
+// round. Pipelined as split_check_phase.
+template <int DC>
+__device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
+                                                 const SplitStore<double>& ms, double* row, int n_tasks,
+                                                 uint32_t n_pad, uint32_t n_bits, float thr_dn, float thr_up,
+                                                 uint32_t* round_word, int wave, int lane) {
+    using qkds::f2;
+    constexpr int NW = kDecodeBlock / 64;
+    int t = wave;
+    if (t >= n_tasks) return;
+    bool bad = false;
+    const uint2* pl = plan + lane;
+    // the row's DC entries past lane 63 are read (times 0) by segments ending
+    // there: keep them finite (the prologue stages key words in this region)
+    if (lane < DC) row[64 + lane] = 0.0;
+    auto slot = [&](uint2 p) -> uint32_t { return pw_row(p) * n_pad + pw_bit(p); };
+    auto edge = [&](double xv, uint2 w) -> double {
+        const f2 bv = qkds::unpack_iv(xv);
+        const bool neg = bv.y < 0.0f;
+        const f2 ab = neg ? -bv.yx : bv;                   // |b2c| in [a, b]
+        // certified sign, magnitude >= 1e-30 (NaN fails); idle lanes (the
+        // dummy column) do not count
+        const bool ok = (neg || bv.x > 0.0f) && ab.x > 1.0e-30f;
+        bad |= !ok && pw_bit(w) != n_bits;
+        const f2 ph = ok ? qkds::phi_bounds(ab.x, ab.y) : f2{0.0f, 0.0f};   // phi(|b2c|)
+        row[lane] = qkds::pack_iv(ph);
+        const uint64_t sgn = __ballot(neg);
+        wave_lds_sync();
+        const int start = pw_start(w);
+        const int deg = pw_deg(w);
+        // extrinsic sum over the other lanes of the segment (a subtraction of
+        // the own term would widen the interval by the own term's width)
+        f2 sum = f2{0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const f2 o = qkds::unpack_iv(row[start + k]);
+            sum = __builtin_elementwise_fma(o, f2((k < deg && start + k != lane) ? 1.0f : 0.0f), sum);
+        }
+        // widened by the binary32 roundings (relative to the sum) and the
+        // reference's binary64 roundings (absolute, qkd_spec.h)
+        const float mg = __builtin_fmaf(sum.y, (float)(deg + 2) * qkds::kSumRel, qkds::kRefSumAbs);
+        f2 ext = sum + f2{-mg, mg};
+        ext.x = ext.x > 0.0f ? ext.x : 0.0f;
+        bad |= !(ext.y < 600.0f);                          // the reference's product would underflow
+        f2 m = qkds::phi_bounds_out(ext.x, ext.y);
+        // threshold_matrix (:246-249) on the magnitude
+        m.x = __builtin_fminf(m.x, thr_dn);
+        m.y = __builtin_fminf(m.y, thr_up);
+        const uint32_t j = pw_chk(w);
+        const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
+        const uint32_t sigma = sj ^ (uint32_t)seg_parity(sgn, w) ^ (neg ? 1u : 0u);
+        return qkds::pack_iv(sigma ? -m.yx : m);
+    };
+    uint2 wa = pl[t * 64];
+    uint2 wb = pl[(t + NW) * 64];
+    double xa = ms.ld(slot(wa));
+    uint32_t pend = 0xffffffffu;
+    double pv = 0;
+    for (;;) {
+        if (pend != 0xffffffffu) ms.st(pend, pv);
+        const uint2 wc = pl[(t + 2 * NW) * 64];
+        const double xb = ms.ld(slot(wb));
+        pv = edge(xa, wa);
+        pend = slot(wa);
+        t += NW;
+        if (t >= n_tasks) break;
+        ms.st(pend, pv);
+        wa = pl[(t + 2 * NW) * 64];
+        xa = ms.ld(slot(wc));
+        pv = edge(xb, wb);
+        pend = slot(wb);
+        t += NW;
+        if (t >= n_tasks) break;
+        wb = wa;
+        wa = wc;
+    }
+    ms.st(pend, pv);
+    if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
+}
+
+// Bit phase on intervals. FOLD (the first iteration): the messages are the
+// exact +-C_d of first_check_phase, so the totals are computed in binary64
+// exactly as the exact path does and the b2c are stored as enclosing
+// intervals. Otherwise: total in L + sum c_k (intervals) and each b2c_k =
+// clamp(total - c2b_k) (:303-316) as the extrinsic sum L + sum_{m != k} c_m, widened by
+// the binary32 and the reference's binary64 rounding allowances, clamped with
+// med3. A hard decision whose sign the interval leaves open marks its checks
+// in xunc (the syndrome test then decides whether the round can stand).
+// Bit degree <= kDvUnroll.
+template <bool FOLD>
+__device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const DecodeArgs& a, const SplitStore<double>& ms,
+                                               const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
+                                               uint32_t* xunc, uint64_t* zw, uint32_t bobmask, bool keep,
+                                               int tid, int wave, int lane) {
+    using qkds::f2;
+    const uint32_t n_pad = (uint32_t)c.n_pad;
+    const double llr_p = a.log_p;
+    const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
+    for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kBitChunk) {
+        double v[kBitChunk][kDvUnroll];
+        int32_t jc[kBitChunk][kDvUnroll];
+        int dg[kBitChunk];
+#pragma unroll
+        for (int u = 0; u < kBitChunk; ++u) {
+            const int i = tid + (r0 + u) * kDecodeBlock;
+            const bool ok = i < c.n;
+            dg[u] = ok ? c.bit_deg[i] : 0;
+            const uint32_t iw = (uint32_t)((r0 + u) * kDecodeBlock + wave * 64);
+#pragma unroll
+            for (int k = 0; k < kDvUnroll; ++k) {
+                const bool ld = ok && k < c.max_dv;
+                v[u][k] = FOLD ? 0.0 : ms.ld_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i);
+                jc[u][k] = ld ? c.bit_chk[k * n_pad + i] : 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kBitChunk; ++u) {
+            const int r = r0 + u;
+            if (r * kDecodeBlock >= c.n) break;            // block-uniform
+            const int i = tid + r * kDecodeBlock;
+            const uint32_t iw = (uint32_t)(r * kDecodeBlock + wave * 64);
+            const bool ok = i < c.n;
+            const int deg = dg[u];
+            const uint32_t bob = (bobmask >> r) & 1u;
+            bool z, unc = false;
+            f2 bo[kDvUnroll];
+            if (FOLD) {
+                // the exact first iteration (fold_first_message, then :256-267, :303-316)
+                const uint32_t sgi = bob ^ lsign;
+                double acc = bob ? -llr_p : llr_p;
+                double cv[kDvUnroll];
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k) {
+                    cv[k] = 0.0;
+                    if (k < deg) {
+                        const int j = jc[u][k];
+                        const uint32_t sp = (qsyn[j >> 5] >> (j & 31)) & 1u;
+                        const double cm = ctab[c.chk_deg[j]];
+                        cv[k] = (sp ^ sgi) ? -cm : cm;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + cv[k] : acc;
+                z = ok && acc <= 0;
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k) bo[k] = qkds::iv_of(clamp_msg(acc - cv[k], a.thr));
+            } else {
+                const f2 L = bob ? f2{-a.lp_up, -a.lp_dn} : f2{a.lp_dn, a.lp_up};
+                f2 cs[kDvUnroll];
+                f2 T = L;
+                float mag = a.lp_up;
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k) {
+                    cs[k] = k < deg ? qkds::unpack_iv(v[u][k]) : f2{0.0f, 0.0f};
+                    T = T + cs[k];
+                    mag = mag + __builtin_fmaxf(__builtin_fabsf(cs[k].x), __builtin_fabsf(cs[k].y));
+                }
+                // binary32 roundings (the sum here and the subtraction below)
+                // and the reference's binary64 ones, relative to the magnitudes
+                const float mg = mag * ((float)(kDvUnroll + 2) * qkds::kSumRel) + 1.0e-30f;
+                T = T + f2{-mg, mg};
+                // z = total <= 0 (:259), certain only if the interval says so
+                const bool z1 = T.y <= 0.0f;
+                unc = ok && !(z1 || T.x > 0.0f);
+                z = ok && z1;
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k) {
+                    // the extrinsic sum L + sum_{m != k} c_m (no dependency widening)
+                    f2 e = L + f2{-mg, mg};
+#pragma unroll
+                    for (int m = 0; m < kDvUnroll; ++m)
+                        if (m != k) e = e + cs[m];
+                    // clamp (:313-316) with binary32 bounds of thr
+                    bo[k] = f2{__builtin_amdgcn_fmed3f(e.x, -a.thr_up, a.thr_dn),
+                               __builtin_amdgcn_fmed3f(e.y, -a.thr_dn, a.thr_up)};
+                }
+            }
+            const uint64_t zb = __ballot(z);
+            if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
+            if (z) {
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k)
+                    if (k < deg) atomicXor(&xsyn[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
+            }
+            if (unc) {
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k)
+                    if (k < deg) atomicOr(&xunc[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
+            }
+            if (!keep || !ok) continue;
+#pragma unroll
+            for (int k = 0; k < kDvUnroll; ++k)
+                if (k < deg) ms.st_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i, qkds::pack_iv(bo[k]));
+        }
+    }
+}
+
 // Flooding sum-product decode of whole frames, one frame per workgroup at a
 // time, frames from the device queue (as decode_kernel). RULE is kRuleSp64
 // (the reference, bit-exact) or kRuleSp32 (the binary32 variant).
-template <int MODE, int RULE, int DC, bool CLAMP>
+//
+// SPEC: the speculative launch (QKD path, binary64 rule, clamp on): frames run
+// interval iterations only; a frame the intervals cannot certify (or that
+// reaches spec_cap, or that the launch's replay policy skips) is appended to
+// a.replay_list for the exact launch that follows, which decodes exactly the
+// listed frames (or every frame when a.replay_list is null).
+template <int MODE, int RULE, int DC, bool CLAMP, bool SPEC>
 __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a) {
     using T = typename RuleMsg<RULE>::T;
     constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
@@ -173,6 +384,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
     uint32_t* qsyn = reinterpret_cast<uint32_t*>(smem + L.qsyn);
+    uint32_t* xunc = reinterpret_cast<uint32_t*>(smem + L.xunc);
     uint64_t* zw = reinterpret_cast<uint64_t*>(smem + L.zw);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
@@ -195,8 +407,13 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     // the fold rebuilds the unrolled rows only)
     const bool fold1 = TABLES && a.first_table && c.max_dv <= kDvUnroll;
     const bool tab2_on = fold1 && a.tab2_entries;
-    uint32_t any_k = 0;
-    if (tid == 0) { ctl[2] = 0; ctl[3] = 0; }
+    uint32_t rnd = 0;    // rounds (iterations of any frame) run by this workgroup
+    if (tid == 0) { ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
+    static_assert(!SPEC || (TABLES && CLAMP), "speculation: QKD path, binary64 rule, clamped messages");
+    // frames of this launch: queue positions < limit; the exact launch after a
+    // speculative one takes the listed frames (written by the previous kernel
+    // on this stream)
+    const uint32_t limit = (!SPEC && a.replay_list) ? *a.replay_count : a.n_frames;
     if (TABLES && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
     if (tab2_on) {
         __syncthreads();
@@ -204,22 +421,42 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     }
     PhaseClock pc(a.phase);
 
+    // frames from the queue: each frame's successor is claimed when the frame
+    // starts (thread 0 keeps it in a register until the frame's end), so the
+    // atomic's round trip overlaps the prologue's loads
+    if (tid == 0) ctl[1] = atomicAdd(a.counter, 1u);
+    uint32_t next_f = 0;
     for (;;) {
         pc.mark(4);
-        if (tid == 0) ctl[0] = atomicAdd(a.counter, 1u);
-        for (int w = tid; w < m_words; w += kDecodeBlock) xsyn[w] = 0;
+        for (int w = tid; w < m_words; w += kDecodeBlock) {
+            xsyn[w] = 0;
+            xunc[w] = 0;
+        }
         __syncthreads();
-        const uint32_t f = ctl[0];
-        if (f >= a.n_frames) break;
+        const uint32_t fq = ctl[1];
+        if (fq >= limit) break;
+        const uint32_t f = (!SPEC && a.replay_list) ? a.replay_list[fq] : fq;
+        if (tid == 0) next_f = atomicAdd(a.counter, 1u);
+        // this launch's replays so far (read now, used for the next frame)
+        uint32_t launch_replays = 0;
+        if (SPEC && tid == 0)
+            launch_replays = __hip_atomic_load(a.replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the speculative launch passes a frame straight to the exact one when
+        // its replay policy says so (ctl[6], set with the frame index)
+        bool replay = SPEC && ctl[6] == 0;
+        if (!replay) {
 
-        // ---- prologue: the frame's Alice and Bob words staged in LDS (the
-        //      product rows are free until the first check phase)
-        const uint64_t* sw = reinterpret_cast<const uint64_t*>(smem + L.tval);   // [alice | bob]
+        // ---- prologue. Keys path: the frame's Bob words staged in LDS (the
+        //      product rows are free until the first check phase) and its
+        //      syndrome words from frame_syn_kernel.
+        const uint64_t* bw = reinterpret_cast<const uint64_t*>(smem + L.tval);
         if (MODE == kModeKeys) {
             uint64_t* w = reinterpret_cast<uint64_t*>(smem + L.tval);
-            for (int q = tid; q < (int)a.words; q += kDecodeBlock) {
-                w[q] = a.alice_w[(size_t)f * a.words + q];
-                w[a.words + q] = a.bob_w[(size_t)f * a.words + q];
+            for (int q = tid; q < (int)a.words; q += kDecodeBlock) w[q] = a.bob_w[(size_t)f * a.words + q];
+            const uint32_t* sy = a.synw + (size_t)f * 2 * m_words;
+            for (int q = tid; q < m_words; q += kDecodeBlock) {
+                tsyn[q] = sy[q];
+                qsyn[q] = sy[m_words + q];
             }
             __syncthreads();
         }
@@ -234,7 +471,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                 if (MODE == kModeLlr) {
                     l = (T)a.llr[(size_t)f * c.n + i];
                 } else {
-                    const uint32_t bb = (uint32_t)((sw[a.words + (i >> 6)] >> (i & 63)) & 1u);
+                    const uint32_t bb = (uint32_t)((bw[i >> 6] >> (i & 63)) & 1u);
                     bobmask |= bb << r;
                     l = bb ? -llr_p : llr_p;
                 }
@@ -247,47 +484,37 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // table index 0 for the second check phase
             if (tid == 0) ms.st((uint32_t)c.n, (T)0);
         }
-        // ---- prologue: target syndrome bits per check (tsyn) and, on the QKD
-        //      path, each check's first-product sign (qsyn); thread per check
-        for (int j0 = wave * 64; j0 < c.m; j0 += kDecodeBlock) {
-            const int j = j0 + lane;
-            const bool ok = j < c.m;
-            int sj = 0, qj = 0;
-            if (MODE == kModeLlr) {
-                sj = ok ? (a.syn[(size_t)f * c.m + j] != 0) : 0;
-            } else {
-                // calculate_syndrome_irregular on Alice's key (:413-414), and
-                // q_j = s_j ^ syn(bob)_j ^ (deg_j & sign(log_p))
-                uint32_t pa = 0, pb = 0, deg = 0;
-                for (int k = 0; k < c.max_dc; ++k) {
-                    const int bit = ok ? c.chk_bits[k * c.m_pad + j] : -1;
-                    if (bit >= 0) {
-                        pa ^= (uint32_t)(sw[bit >> 6] >> (bit & 63));
-                        pb ^= (uint32_t)(sw[a.words + (bit >> 6)] >> (bit & 63));
-                        deg++;
-                    }
+        // ---- prologue, LLR path: target syndrome bits per check (tsyn), thread per check
+        if (MODE == kModeLlr) {
+            for (int j0 = wave * 64; j0 < c.m; j0 += kDecodeBlock) {
+                const int j = j0 + lane;
+                const int sj = j < c.m ? (a.syn[(size_t)f * c.m + j] != 0) : 0;
+                const uint64_t sm = __ballot(sj);
+                if (lane == 0) {
+                    tsyn[j0 >> 5] = (uint32_t)sm;
+                    tsyn[(j0 >> 5) + 1] = (uint32_t)(sm >> 32);
                 }
-                sj = (int)(pa & 1u);
-                qj = (int)((pa ^ pb ^ (lsign & deg)) & 1u);
-            }
-            const uint64_t sm = __ballot(sj);
-            const uint64_t qm = __ballot(qj);
-            if (lane == 0) {
-                tsyn[j0 >> 5] = (uint32_t)sm;
-                tsyn[(j0 >> 5) + 1] = (uint32_t)(sm >> 32);
-                qsyn[j0 >> 5] = (uint32_t)qm;
-                qsyn[(j0 >> 5) + 1] = (uint32_t)(qm >> 32);
             }
         }
         __syncthreads();
         pc.mark(0);
 
-        // ---- iterations (:212-330)
+        // ---- iterations (:212-330): interval iterations (qkd_spec.h) in the
+        //      speculative launch, the reference's binary64 ones otherwise
+        constexpr bool spec = SPEC;
         bool done = false;
         uint32_t it = 0;
-        for (; it < a.max_it; ++it) {
+        for (;;) {
+            if (it >= a.max_it) break;
             const bool folded = fold1 && it == 0;
-            if (!folded) {
+            uint32_t* rw = ctl + 4 + (rnd & 1u);
+            if constexpr (SPEC) {
+                if (!folded) {
+                    spec_check_phase<DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn, a.thr_up,
+                                         rw, wave, lane);
+                    __syncthreads();
+                }
+            } else if (!folded) {
                 if (TABLES && it == 1 && tab2_on)
                     split_check_phase<kSrcTable, CLAMP, DC, RULE>(c.plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);
@@ -302,6 +529,12 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
             // the hard decision's syndrome (:277, calculate_syndrome_irregular :476-486),
             // then b2c_k = clamp(total_i - c2b_k) (:303-316) into slot k.
+            if constexpr (SPEC) {
+                if (folded)
+                    spec_bit_phase<true>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
+                else
+                    spec_bit_phase<false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
+            } else
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kBitChunk) {
                 T v[kBitChunk][kDvUnroll];
                 int32_t jc[kBitChunk][kDvUnroll];
@@ -403,55 +636,194 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             }
             __syncthreads();
             pc.mark(2);
+            // round flags: bit 0 a check certainly unsatisfied, bit 1 speculation
+            // abort, bit 2 some check's parity uncertain (speculative rounds).
+            // The next round's word was last read before this round's phases
+            // and is next written after the barrier below.
+            if (tid == 0) ctl[4 + ((rnd + 1) & 1u)] = 0;
             // syndrome test (:285): any word differing from the target
-            bool mismatch = false;
+            bool mismatch = false, uncertain = false;
             for (int w = tid; w < m_words; w += kDecodeBlock) {
-                mismatch |= xsyn[w] != tsyn[w];
+                const uint32_t u = xunc[w];
+                mismatch |= ((xsyn[w] ^ tsyn[w]) & ~u) != 0;
+                uncertain |= u != 0;
                 xsyn[w] = 0;
+                xunc[w] = 0;
             }
-            const bool any_mismatch = block_any(mismatch, ctl + 2, any_k);
+            const uint32_t wv = __builtin_amdgcn_readfirstlane(
+                (uint32_t)(__any(mismatch) ? 1u : 0u) | (uint32_t)(__any(uncertain) ? 4u : 0u));
+            if (wv && lane == 0) atomicOr(rw, wv);
+            __syncthreads();
+            const uint32_t fl = *rw;
+            rnd++;
             pc.mark(3);
+            // A speculative round stands if no sign was lost on the way (bit 1)
+            // and its outcome is certain: a certainly unsatisfied check (bit 0;
+            // the reference iterates on), unless this was the last iteration,
+            // whose hard decision is the output and must then be certain too;
+            // or no uncertainty at all (bit 2 clear: the decision is exact).
+            if (spec && ((fl & 2u) || ((fl & 4u) && (!(fl & 1u) || it + 1 >= a.max_it)))) {
+                replay = true;          // decode the frame exactly (next launch)
+                break;
+            }
 #ifndef QKD_EXP_NO_STOP
-            if (!any_mismatch) {
+            if (!(fl & 1u)) {
                 done = true;
                 break;
             }
 #endif
-        }
-
-        // ---- outputs: SP_result + last hard decision (+ keys_match)
-        bool key_mismatch = false;
-        for (int i = tid; i < c.n; i += kDecodeBlock) {
-            const uint8_t d = (uint8_t)((zw[i >> 6] >> (i & 63)) & 1u);
-            if (a.bits_out) a.bits_out[(size_t)f * c.n + i] = d;
-            if (MODE == kModeKeys) {
-                const uint64_t w = a.alice_w[(size_t)f * a.words + (i >> 6)];
-                key_mismatch |= (uint8_t)((w >> (i & 63)) & 1u) != d;
+            ++it;
+            if (spec && it >= a.spec_cap && it < a.max_it) {
+                replay = true;
+                break;
             }
         }
-        if (MODE == kModeKeys) {
-            __syncthreads();
-            const bool km = block_any(key_mismatch, ctl + 2, any_k);
-            if (tid == 0 && a.key_ok) a.key_ok[f] = km ? 0 : 1;   // arrays_equal (:433)
+
+        // ---- outputs: SP_result and the last hard decision (keys path:
+        //      packed, for key_match_kernel's arrays_equal, :433)
+        if (!replay) {
+            if (MODE == kModeKeys) {
+                for (int q = tid; q < (int)a.words; q += kDecodeBlock) a.zout[(size_t)f * a.words + q] = zw[q];
+            } else if (a.bits_out) {
+                for (int i = tid; i < c.n; i += kDecodeBlock)
+                    a.bits_out[(size_t)f * c.n + i] = (uint8_t)((zw[i >> 6] >> (i & 63)) & 1u);
+            }
+            if (tid == 0) {
+                a.iters[f] = done ? it + 1 : a.max_it;
+                a.sp_ok[f] = done ? 1 : 0;
+            }
         }
+        }   // !replay on entry
         if (tid == 0) {
-            a.iters[f] = done ? it + 1 : a.max_it;
-            a.sp_ok[f] = done ? 1 : 0;
+            if (SPEC && replay) {
+                a.replay_list[atomicAdd(a.replay_count, 1u)] = f;
+                atomicAdd(a.spec_replays, 1ull);
+            }
+            ctl[1] = next_f;
+            // speculate on the next frame unless a quarter of the frames
+            // started so far (past the first 64) were replayed
+            ctl[6] = launch_replays * 4u <= next_f + 64u ? 1u : 0u;
         }
         __syncthreads();
     }
     pc.flush();
 }
 
-template <int MODE, int RULE, bool CLAMP>
-static DecodeFn pick_split_dc(int max_dc, int* dc) {
-    if (max_dc <= 4) { *dc = 4; return decode_split_kernel<MODE, RULE, 4, CLAMP>; }
-    if (max_dc <= 6) { *dc = 6; return decode_split_kernel<MODE, RULE, 6, CLAMP>; }
-    if (max_dc <= 8) { *dc = 8; return decode_split_kernel<MODE, RULE, 8, CLAMP>; }
-    if (max_dc <= 16) { *dc = 16; return decode_split_kernel<MODE, RULE, 16, CLAMP>; }
-    *dc = 64;
-    return decode_split_kernel<MODE, RULE, 64, CLAMP>;
+// ---- keys path: the kernels around decode_split_kernel ---------------------
+// frame_syn_kernel: per frame the target syndrome s_A = H * alice
+// (calculate_syndrome_irregular, array_and_matrix_operations.cpp:476-486, on
+// Alice's key, qkd_ldpc_algorithm.cpp:413-414) and the sign of each check's
+// first-iteration product, q_j = s_j ^ (H * bob)_j ^ (deg_j & sign(log_p))
+// (first_check_phase), one bit per check in whole 64-check groups. kSynFrames
+// frames per workgroup share each load of a check's row.
+constexpr int kSynFrames = 8;
+constexpr int kSynBlock = 256;
+__global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, const uint64_t* __restrict__ alice_w,
+                                                              const uint64_t* __restrict__ bob_w, uint32_t words,
+                                                              uint32_t n_frames, uint32_t lsign, uint32_t* synw) {
+    extern __shared__ uint64_t kw[];   // [kSynFrames][alice | bob][words]
+    const uint32_t f0 = blockIdx.x * kSynFrames;
+    const uint32_t nf = min((uint32_t)kSynFrames, n_frames - f0);
+    for (uint32_t q = threadIdx.x; q < nf * words; q += kSynBlock) {
+        const uint32_t fr = q / words;
+        const uint32_t w = q - fr * words;
+        kw[(2 * fr) * words + w] = alice_w[(size_t)(f0 + fr) * words + w];
+        kw[(2 * fr + 1) * words + w] = bob_w[(size_t)(f0 + fr) * words + w];
+    }
+    __syncthreads();
+    const int m_words = decode_m_words(c.m);
+    const int lane = threadIdx.x & 63;
+    for (int j0 = (int)(threadIdx.x & ~63u); j0 < c.m; j0 += kSynBlock) {
+        const int j = j0 + lane;
+        uint32_t pa[kSynFrames], pb[kSynFrames];
+#pragma unroll
+        for (int fr = 0; fr < kSynFrames; ++fr) pa[fr] = pb[fr] = 0;
+        uint32_t deg = 0;
+        if (j < c.m) {
+            for (int k = 0; k < c.max_dc; ++k) {
+                const int bit = c.chk_bits[k * c.m_pad + j];
+                if (bit < 0) continue;
+                deg++;
+                const uint32_t wi = (uint32_t)bit >> 6, sh = (uint32_t)bit & 63u;
+#pragma unroll
+                for (int fr = 0; fr < kSynFrames; ++fr) {
+                    pa[fr] ^= (uint32_t)(kw[(2 * fr) * words + wi] >> sh);
+                    pb[fr] ^= (uint32_t)(kw[(2 * fr + 1) * words + wi] >> sh);
+                }
+            }
+        }
+#pragma unroll
+        for (int fr = 0; fr < kSynFrames; ++fr) {
+            const uint64_t sm = __ballot(pa[fr] & 1u);
+            const uint64_t qm = __ballot((pa[fr] ^ pb[fr] ^ (lsign & deg)) & 1u);
+            if (lane == 0 && (uint32_t)fr < nf) {
+                uint32_t* o = synw + (size_t)(f0 + fr) * 2 * m_words;
+                o[j0 >> 5] = (uint32_t)sm;
+                o[(j0 >> 5) + 1] = (uint32_t)(sm >> 32);
+                o[m_words + (j0 >> 5)] = (uint32_t)qm;
+                o[m_words + (j0 >> 5) + 1] = (uint32_t)(qm >> 32);
+            }
+        }
+    }
 }
+
+// key_match_kernel: keys_match = arrays_equal(alice, decoded) (:433, :96-106),
+// one wave per frame over the packed words.
+__global__ __launch_bounds__(64) void key_match_kernel(const uint64_t* __restrict__ zout,
+                                                       const uint64_t* __restrict__ alice_w, uint32_t n,
+                                                       uint32_t words, uint8_t* key_ok) {
+    const uint32_t f = blockIdx.x;
+    bool mis = false;
+    for (uint32_t q = threadIdx.x; q < words; q += 64) {
+        uint64_t d = zout[(size_t)f * words + q] ^ alice_w[(size_t)f * words + q];
+        if ((q + 1) * 64 > n) d &= (1ull << (n - q * 64)) - 1ull;
+        mis |= d != 0;
+    }
+    const bool any = __any(mis);
+    if (threadIdx.x == 0) key_ok[f] = any ? 0 : 1;
+}
+
+__global__ void zout_unpack_kernel(const uint64_t* zout, uint32_t n, uint32_t words, uint32_t n_frames,
+                                   uint8_t* out) {
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (size_t)n_frames * n) return;
+    const size_t f = gid / n;
+    const uint32_t i = (uint32_t)(gid - f * n);
+    out[gid] = (uint8_t)((zout[f * words + (i >> 6)] >> (i & 63)) & 1u);
+}
+
+hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
+    const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
+    const size_t lds = (size_t)kSynFrames * 2 * a.words * sizeof(uint64_t);
+    hipLaunchKernelGGL(frame_syn_kernel, dim3((a.n_frames + kSynFrames - 1) / kSynFrames), dim3(kSynBlock), lds,
+                       stream, a.code, a.alice_w, a.bob_w, a.words, a.n_frames, lsign,
+                       const_cast<uint32_t*>(a.synw));
+    return hipGetLastError();
+}
+
+hipError_t launch_key_match(const DecodeArgs& a, hipStream_t stream) {
+    if (a.key_ok)
+        hipLaunchKernelGGL(key_match_kernel, dim3(a.n_frames), dim3(64), 0, stream, a.zout, a.alice_w,
+                           (uint32_t)a.code.n, a.words, a.key_ok);
+    if (a.bits_out) {
+        const size_t total = (size_t)a.n_frames * a.code.n;
+        hipLaunchKernelGGL(zout_unpack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, a.zout,
+                           (uint32_t)a.code.n, a.words, a.n_frames, a.bits_out);
+    }
+    return hipGetLastError();
+}
+
+template <int MODE, int RULE, bool CLAMP, bool SPEC = false>
+static DecodeFn pick_split_dc(int max_dc, int* dc) {
+    if (max_dc <= 4) { *dc = 4; return decode_split_kernel<MODE, RULE, 4, CLAMP, SPEC>; }
+    if (max_dc <= 6) { *dc = 6; return decode_split_kernel<MODE, RULE, 6, CLAMP, SPEC>; }
+    if (max_dc <= 8) { *dc = 8; return decode_split_kernel<MODE, RULE, 8, CLAMP, SPEC>; }
+    if (max_dc <= 16) { *dc = 16; return decode_split_kernel<MODE, RULE, 16, CLAMP, SPEC>; }
+    *dc = 64;
+    return decode_split_kernel<MODE, RULE, 64, CLAMP, SPEC>;
+}
+
+DecodeFn pick_split_spec(int max_dc, int* dc) { return pick_split_dc<kModeKeys, kRuleSp64, true, true>(max_dc, dc); }
 
 template <int MODE, int RULE>
 static DecodeFn pick_split_clamp(bool clamp, int max_dc, int* dc) {

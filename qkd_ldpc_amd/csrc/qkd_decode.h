@@ -12,6 +12,10 @@
 namespace qkd {
 
 
+// Speculative interval iterations per frame before the exact fallback
+// (decode_split.hip; QKD_SPEC_CAP overrides).
+constexpr int kSpecCapDefault = 8;
+
 // Largest check degree the first-iteration table covers.
 constexpr int kFirstTableDeg = 16;
 
@@ -80,6 +84,24 @@ struct DecodeArgs {
     size_t totals_stride;
     // decode_split_kernel: the LDS budget its layout was sized for (SplitLds)
     uint32_t lds_budget;
+    // decode_split_kernel, kModeKeys: per frame 2 * m_words syndrome words
+    // from frame_syn_kernel (target s_A, then the first-product signs), and
+    // the frame's last hard decision out as packed words (key_match_kernel
+    // compares them with Alice's key and unpacks bits_out)
+    const uint32_t* synw;
+    uint64_t* zout;
+    // decode_split_kernel, kModeKeys, binary64 rule: speculative interval
+    // iterations (qkd_spec.h) before the exact ones; spec_cap = how many (0:
+    // off), log_p and thr as binary32 bounds, spec_replays counts the frames
+    // that fell back to the exact iterations
+    uint32_t spec_cap;
+    float lp_dn, lp_up, thr_dn, thr_up;
+    unsigned long long* spec_replays;
+    // the frames the speculative launch leaves to the exact one: the list and
+    // its length (zeroed per call); once the list passes a quarter of the
+    // frames started, the remaining frames skip the speculation
+    uint32_t* replay_list;
+    uint32_t* replay_count;
 };
 
 // Phase-clock accumulation (diagnostic; a wave-uniform test when off). Each
@@ -344,18 +366,19 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 // ---- split message store (decode_split.hip) ----------------------------------
 // LDS layout of decode_split_kernel (bytes):
 //   tsyn, xsyn, qsyn [m_words]   target syndrome / XOR-built syndrome / first-product signs
+//   xunc  [m_words]              speculative rounds: checks with an uncertain hard decision
 //   zw    [n_pad / 64] uint64    hard decision of the last bit phase, one bit per bit
 //   tval  [NW][64 + DC] T        per-wave rows for the in-check products
 //                                (prologue: the frame's Alice + Bob words)
 //   ctab  [kFirstTableDeg + 1]   first-iteration message magnitudes by degree
 //   tab2  [tab2_entries]         second-iteration tanh table
-//   ctl   [4]                    frame index, block_any flags
+//   ctl   [8]                    [1] next frame, [4..5] round flags (decode_split.hip)
 //   msg   [S + 64] T             message slots 0 .. S-1 (slots S .. max_dv*n_pad-1
 //                                live in the workgroup's global region), then
 //                                one trash slot per lane
 // S is as many slots as the budget leaves after the rest.
 struct SplitLds {
-    size_t tsyn, xsyn, qsyn, zw, tval, ctab, tab2, ctl, msg, bytes;
+    size_t tsyn, xsyn, qsyn, xunc, zw, tval, ctab, tab2, ctl, msg, bytes;
     uint32_t S;
     __host__ __device__ SplitLds(int n_pad, int n_words, int m, int max_dv, int dc, int tab2_entries, int esz,
                                  size_t budget) {
@@ -363,14 +386,15 @@ struct SplitLds {
         tsyn = 0;
         xsyn = tsyn + (size_t)m_words * 4;
         qsyn = xsyn + (size_t)m_words * 4;
-        zw = (qsyn + (size_t)m_words * 4 + 15) & ~(size_t)15;
+        xunc = qsyn + (size_t)m_words * 4;
+        zw = (xunc + (size_t)m_words * 4 + 15) & ~(size_t)15;
         tval = (zw + (size_t)(n_pad / 64) * 8 + 15) & ~(size_t)15;
         const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * esz;
         const size_t stage = (size_t)n_words * 16;
         ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         ctl = (tab2 + (size_t)tab2_entries * 8 + 15) & ~(size_t)15;
-        msg = ctl + 16;
+        msg = ctl + 32;
         const size_t slots = (size_t)max_dv * n_pad;
         // 64 trash slots follow the S message slots (decode_split.hip SplitStore)
         const size_t fit = budget > msg + 64 * (size_t)esz ? (budget - msg) / (size_t)esz - 64 : 0;
@@ -383,5 +407,11 @@ using DecodeFn = void (*)(DecodeArgs);
 // decode_split.hip: the split-store kernel for (mode, rule in {kRuleSp64,
 // kRuleSp32}, clamp, check-degree bucket); *dc receives the bucket.
 DecodeFn pick_split_decode(int mode, int rule, bool clamp, int max_dc, int* dc);
+// The speculative launch of the QKD path (binary64 rule, clamp on).
+DecodeFn pick_split_spec(int max_dc, int* dc);
+// decode_split.hip, kModeKeys: the kernels around the split decoder.
+// Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.
+hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream);
+hipError_t launch_key_match(const DecodeArgs& a, hipStream_t stream);
 
 }  // namespace qkd

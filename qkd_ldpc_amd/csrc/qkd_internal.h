@@ -76,6 +76,12 @@ struct qkd_workspace {
     uint64_t* alice_w = nullptr;
     uint64_t* bob_w = nullptr;
     size_t key_frames = 0;
+    // split decoder, keys path (decode_split.hip): per frame the target and
+    // first-product syndrome words (frame_syn_kernel) and the hard decision
+    // words the decoder leaves for key_match_kernel; sized with the keys
+    uint32_t* synw = nullptr;
+    uint64_t* zout = nullptr;
+    uint32_t* replay = nullptr;     // frames the speculative launch leaves to the exact one
     // keygen shuffle scratch (ne words per frame)
     uint32_t* low = nullptr;
     size_t low_words = 0;

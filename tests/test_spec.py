@@ -1,0 +1,158 @@
+"""Speculative interval iterations (qkd_ldpc_amd/csrc/qkd_spec.h, decode_split.hip).
+
+The QKD path first decodes each frame with binary32 intervals that must contain
+the reference's binary64 messages; a frame whose hard decisions the intervals
+cannot certify is decoded again exactly. Outputs must be bit-exact either way:
+every comparison below is exact (iteration counts, flags, decoded bits), against
+the golden vectors of the pinned oracle or the oracle itself, at several caps
+(QKD_SPEC_CAP; 0 = exact iterations only).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def Q():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    import qkd_ldpc_amd as Q
+    return Q
+
+
+@pytest.fixture(scope="module")
+def H(Q, golden_code):
+    return Q.HMatrix.from_check_lists(int(golden_code["dims"][0]), golden_code["chk_off"],
+                                      golden_code["chk_idx"])
+
+
+def seeds_dev(seeds):
+    return torch.from_numpy(np.ascontiguousarray(seeds, np.uint64).view(np.int64)).cuda()
+
+
+def phi64(x):
+    """phi(x) = -ln tanh(x/2) = log1p(2u / (1 - u)), u = e^-x, in binary64."""
+    x = np.asarray(x, np.float64)
+    u = np.exp(-x)
+    return np.log1p(2.0 * u / -np.expm1(-x))
+
+
+def replays(Q, ws, reset=True):
+    v = C.c_uint64(0)
+    Q._native.check(Q._native.lib().qkd_debug_spec_replays(ws.handle, C.byref(v), int(reset)))
+    return v.value
+
+
+def device_phi(Q, which, a, b):
+    x = np.empty(2 * a.size, np.float64)
+    x[0::2] = a
+    x[1::2] = b
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.empty_like(dx)
+    Q._native.check(Q._native.lib().qkd_debug_math(which, dx.data_ptr(), dy.data_ptr(), dx.numel(), None))
+    torch.cuda.synchronize()
+    y = dy.cpu().numpy()
+    return y[0::2], y[1::2]
+
+
+@pytest.mark.parametrize("rel", [0.0, 1e-7, 1e-5, 1e-3, 0.5])
+def test_phi_bounds_contain_phi(Q, rel):
+    """phi_bounds (input side) and phi_bounds_out (output side) bracket phi over
+    [a, b] for a dense sweep of a (binary32) in [1e-30, 120]; the value checked is
+    phi at both ends (phi is monotone, so the ends are its extremes)."""
+    rng = np.random.default_rng(7)
+    a = np.concatenate([
+        np.exp(rng.uniform(np.log(1e-30), np.log(120.0), 1000000)),
+        rng.uniform(0.0, 5.0, 1000000),
+        np.array([0.35, 2.0, 4.0, 80.0, 1.0, 0.5], np.float64),
+    ]).astype(np.float32).astype(np.float64)
+    b = (a * (1.0 + rel)).astype(np.float32).astype(np.float64)
+    b = np.maximum(a, b)
+    for which in (4, 5):
+        lo, hi = device_phi(Q, which, a, b)
+        pa, pb = phi64(a), phi64(b)
+        assert (lo <= pb).all(), (which, a[lo > pb][:5], lo[lo > pb][:5], pb[lo > pb][:5])
+        assert (hi >= pa).all(), (which, a[hi < pa][:5], hi[hi < pa][:5], pa[hi < pa][:5])
+        assert (lo >= 0).all()
+        if rel == 0.0:
+            fin0 = (a < 70) & (pa > 1e-30)
+            # headroom: how much of the 2^-20 allowance the evaluation uses
+            # (hi = phi~ (1 + 2^-20), phi~ the evaluation)
+            R = 2.0 ** -20
+            err = np.abs(hi[fin0] / (1.0 + R) / pa[fin0] - 1.0)
+            k = int(np.argmax(err))
+            print(f"phi form {which}: max relative evaluation error {err[k]:.3g} at x = {a[fin0][k]:.6g} "
+                  f"({err[k] / R:.2f} of the allowance)")
+            assert err[k] < 0.5 * R
+
+
+def test_phi_bounds_out_at_zero(Q):
+    """A phi-domain sum that may be 0 (the reference's P / t can be exactly +-1)
+    has an infinite upper bound."""
+    a = np.array([0.0, 0.0, 1e-14], np.float64)
+    b = np.array([1e-14, 3.0, 2e-14], np.float64)
+    lo, hi = device_phi(Q, 5, a, b)
+    assert np.isinf(hi[0]) and np.isinf(hi[1]) and np.isfinite(hi[2])
+    assert (lo <= phi64(b)).all()
+
+
+@pytest.mark.parametrize("cap", ["0", "1", "2", "3", "8", "50"])
+def test_trials_config2_every_cap(Q, H, golden_vectors, monkeypatch, cap):
+    monkeypatch.setenv("QKD_SPEC_CAP", cap)
+    seeds = seeds_dev(Q.make_seeds(777, 4096))
+    ws = Q.Workspace(H)
+    replays(Q, ws)
+    r = Q.run_trials(H, seeds, 0.02, 0, 50, 100.0, True, workspace=ws)
+    torch.cuda.synchronize()
+    assert (r.iterations.cpu().numpy() == golden_vectors["c2_iters"]).all()
+    assert (r.syndromes_match.cpu().numpy().astype(bool) == golden_vectors["c2_sp"]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c2_ko"]).all()
+    n = replays(Q, ws)
+    print(f"cap {cap}: {n} of 4096 frames replayed exactly")
+    if cap == "8":
+        assert n < 4096 // 10          # the intervals certify almost every frame
+
+
+@pytest.mark.parametrize("cap", ["2", "8", "50"])
+def test_trials_config3_points_every_cap(Q, H, golden_vectors, monkeypatch, cap):
+    monkeypatch.setenv("QKD_SPEC_CAP", cap)
+    seeds = seeds_dev(Q.make_seeds(777, 10000))
+    ws = Q.Workspace(H)
+    grid = golden_vectors["c3_qnom"]
+    for s, qn in enumerate(grid):
+        replays(Q, ws)
+        r = Q.run_trials(H, seeds, float(qn), s, 50, 100.0, True, workspace=ws)
+        torch.cuda.synchronize()
+        assert (r.iterations.cpu().numpy() == golden_vectors["c3_iters"][s]).all(), (cap, s)
+        assert (r.syndromes_match.cpu().numpy().astype(bool) == golden_vectors["c3_sp"][s]).all()
+        assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c3_ko"][s]).all()
+        print(f"cap {cap} q {qn:.2f}: {replays(Q, ws)} of 10000 replayed")
+
+
+@pytest.mark.parametrize("q,max_it", [(0.05, 50), (0.09, 50), (0.11, 12), (0.15, 6)])
+@pytest.mark.parametrize("thr", [100.0, 2.5, 0.7])
+def test_spec_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, thr):
+    """Decoded words of converging and failing frames (the cap at max_it lets the
+    speculative iterations run to the end) equal the oracle's bit for bit."""
+    monkeypatch.setenv("QKD_SPEC_CAP", "64")
+    rng = np.random.default_rng(int(q * 1000) + int(thr * 10))
+    f = 4
+    alice = rng.integers(0, 2, (f, 10240))
+    bob = alice ^ (rng.random((f, 10240)) < q)
+    r = Q.qkd_ldpc(H, torch.from_numpy(alice.astype(np.uint8)).cuda(),
+                   torch.from_numpy(bob.astype(np.uint8)).cuda(), q, max_it, thr, True, want_bits=True)
+    torch.cuda.synchronize()
+    its = r.iterations.cpu().numpy()
+    sp = r.syndromes_match.cpu().numpy()
+    ko = r.keys_match.cpu().numpy()
+    bits = r.bits.cpu().numpy()
+    for k in range(f):
+        want = oracle_code.qkd_ldpc(alice[k], bob[k], q, max_it, thr, True)
+        assert its[k] == want["iters"], (q, thr, k)
+        assert bool(sp[k]) == want["sp_ok"] and bool(ko[k]) == want["key_ok"]
+        assert (bits[k] == want["out"]).all(), (q, thr, k)
