@@ -979,16 +979,14 @@ qkd_status ws_reserve_keys(qkd_workspace* ws, size_t frames, size_t low_words) {
         if (ws->bob_w) QKD_HIP(hipFree(ws->bob_w));
         if (ws->synw) QKD_HIP(hipFree(ws->synw));
         if (ws->zout) QKD_HIP(hipFree(ws->zout));
-        if (ws->replay) QKD_HIP(hipFree(ws->replay));
         ws->alice_w = ws->bob_w = ws->zout = nullptr;
-        ws->synw = ws->replay = nullptr;
+        ws->synw = nullptr;
         ws->key_frames = 0;
         const size_t syn_words = 2 * (size_t)decode_m_words(c->m);
         if (hipMalloc(&ws->alice_w, frames * words * 8) != hipSuccess ||
             hipMalloc(&ws->bob_w, frames * words * 8) != hipSuccess ||
             hipMalloc(&ws->synw, frames * syn_words * 4) != hipSuccess ||
-            hipMalloc(&ws->zout, frames * words * 8) != hipSuccess ||
-            hipMalloc(&ws->replay, frames * 4) != hipSuccess)
+            hipMalloc(&ws->zout, frames * words * 8) != hipSuccess)
             return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate keys for %zu frames", frames);
         ws->key_frames = frames;
     }
@@ -1011,8 +1009,10 @@ static qkd_status ws_free(qkd_workspace* ws) {
     if (ws->bob_w) (void)hipFree(ws->bob_w);
     if (ws->synw) (void)hipFree(ws->synw);
     if (ws->zout) (void)hipFree(ws->zout);
-    if (ws->replay) (void)hipFree(ws->replay);
     if (ws->low) (void)hipFree(ws->low);
+    if (ws->spec_stat_ev) (void)hipEventSynchronize(ws->spec_stat_ev);
+    if (ws->spec_stat_host) (void)hipHostFree(ws->spec_stat_host);
+    if (ws->spec_stat_ev) (void)hipEventDestroy(ws->spec_stat_ev);
     if (ws->done) (void)hipEventDestroy(ws->done);
     return QKD_OK;
 }
@@ -1083,16 +1083,13 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             a.c2b_stride = (slots - L.S + 31) & ~(size_t)31;      // elements of the message type
             a.lds_budget = (uint32_t)budget;
             a.counter = ws->counter;
-            // [0] frame queue of the first launch, [1] replay list length,
-            // [2] frame queue of the exact launch after a speculative one
-            QKD_HIP(hipMemsetAsync(ws->counter, 0, 12, stream));
+            QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));     // [0] frame queue, [1] replays
             static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;
             a.phase = nullptr;
             if (timing) {
                 a.phase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 64);
                 QKD_HIP(hipMemsetAsync(a.phase, 0, 64, stream));
             }
-            a.replay_list = nullptr;
             a.replay_count = ws->counter + 1;
             if (mode == kModeKeys) {
                 a.synw = ws->synw;
@@ -1100,21 +1097,18 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 a.spec_replays = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 120);
                 QKD_HIP(launch_frame_syn(a, stream));
             }
-            // speculative interval iterations (qkd_spec.h) first, when they
-            // apply: QKD path with the folded first iteration, binary64 rule,
-            // clamped messages, bit degree <= kDvUnroll
+            // the speculative kernel (interval iterations, qkd_spec.h, exact
+            // replays in place) when it applies: QKD path with the folded first
+            // iteration, binary64 rule, clamped messages, bit degree <= kDvUnroll
             const bool spec = mode == kModeKeys && rule == kRuleSp64 && a.spec_cap > 0 && a.clamp_on &&
-                              a.first_table && c->max_dv <= kDvUnroll && ws->replay;
+                              a.first_table && c->max_dv <= kDvUnroll;
             if (spec) {
                 int xdc = 0, sgrid = 0;
                 DecodeFn xfn = pick_split_spec(c->max_dc, &xdc);
                 s = decode_grid(c, xfn, L.bytes, &sgrid);
                 if (s != QKD_OK) return s;
-                sgrid = std::min(sgrid, grid);
-                a.replay_list = ws->replay;
-                hipLaunchKernelGGL(xfn, dim3(sgrid), dim3(kDecodeBlock), L.bytes, stream, a);
-                QKD_HIP(hipGetLastError());
-                a.counter = ws->counter + 2;      // the exact launch takes the listed frames
+                sfn = xfn;
+                grid = std::min(sgrid, grid);
             }
             hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
             QKD_HIP(hipGetLastError());
@@ -1294,7 +1288,29 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     a.iters = iters;
     a.sp_ok = sp_ok;
     a.key_ok = key_ok;
-    return launch_decode(c, ws, a, kModeKeys, flags, stream);
+    // across calls: the last speculative call's replay fraction, once its
+    // count is back (never waits); above kSpecReplayMax the speculation stays
+    // off from that QBER up
+    if (ws->spec_stat_pending && hipEventQuery(ws->spec_stat_ev) == hipSuccess) {
+        ws->spec_stat_pending = false;
+        if ((double)*ws->spec_stat_host > kSpecReplayMax * (double)ws->spec_stat_frames)
+            ws->spec_off_q = std::min(ws->spec_off_q, ws->spec_stat_q);
+    }
+    if (q >= ws->spec_off_q) a.spec_cap = 0;
+    qkd_status st = launch_decode(c, ws, a, kModeKeys, flags, stream);
+    if (st != QKD_OK || a.spec_cap == 0 || ws->spec_stat_pending) return st;
+    if (!ws->spec_stat_host) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&ws->spec_stat_host), 8, hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&ws->spec_stat_ev, hipEventDisableTiming) != hipSuccess)
+            return QKD_OK;                        // no policy feedback, decoding is unaffected
+    }
+    if (hipMemcpyAsync(ws->spec_stat_host, ws->counter + 1, 4, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+        hipEventRecord(ws->spec_stat_ev, stream) == hipSuccess) {
+        ws->spec_stat_pending = true;
+        ws->spec_stat_q = q;
+        ws->spec_stat_frames = n_frames;
+    }
+    return QKD_OK;
 }
 
 qkd_status qkd_qkd_ldpc_batch(const qkd_code* c, qkd_workspace* ws, const uint8_t* alice,

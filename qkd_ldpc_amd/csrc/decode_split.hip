@@ -368,11 +368,12 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
 // time, frames from the device queue (as decode_kernel). RULE is kRuleSp64
 // (the reference, bit-exact) or kRuleSp32 (the binary32 variant).
 //
-// SPEC: the speculative launch (QKD path, binary64 rule, clamp on): frames run
-// interval iterations only; a frame the intervals cannot certify (or that
-// reaches spec_cap, or that the launch's replay policy skips) is appended to
-// a.replay_list for the exact launch that follows, which decodes exactly the
-// listed frames (or every frame when a.replay_list is null).
+// SPEC (QKD path, binary64 rule, clamp on): each frame first runs interval
+// iterations (qkd_spec.h); a frame the intervals cannot certify (or that
+// reaches spec_cap) restarts at once with the exact iterations, which this
+// instantiation compiles with a shorter bit-phase load batch (kBitChunkSpec)
+// to leave the registers to the interval phases. The replay policy (ctl[6])
+// can send a frame straight to the exact iterations.
 template <int MODE, int RULE, int DC, bool CLAMP, bool SPEC>
 __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a) {
     using T = typename RuleMsg<RULE>::T;
@@ -410,10 +411,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     uint32_t rnd = 0;    // rounds (iterations of any frame) run by this workgroup
     if (tid == 0) { ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
     static_assert(!SPEC || (TABLES && CLAMP), "speculation: QKD path, binary64 rule, clamped messages");
-    // frames of this launch: queue positions < limit; the exact launch after a
-    // speculative one takes the listed frames (written by the previous kernel
-    // on this stream)
-    const uint32_t limit = (!SPEC && a.replay_list) ? *a.replay_count : a.n_frames;
+    constexpr int BC = SPEC ? kBitChunkSpec : kBitChunk;      // exact bit phase load batch
     if (TABLES && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
     if (tab2_on) {
         __syncthreads();
@@ -433,18 +431,13 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             xunc[w] = 0;
         }
         __syncthreads();
-        const uint32_t fq = ctl[1];
-        if (fq >= limit) break;
-        const uint32_t f = (!SPEC && a.replay_list) ? a.replay_list[fq] : fq;
+        const uint32_t f = ctl[1];
+        if (f >= a.n_frames) break;
         if (tid == 0) next_f = atomicAdd(a.counter, 1u);
         // this launch's replays so far (read now, used for the next frame)
         uint32_t launch_replays = 0;
         if (SPEC && tid == 0)
             launch_replays = __hip_atomic_load(a.replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // the speculative launch passes a frame straight to the exact one when
-        // its replay policy says so (ctl[6], set with the frame index)
-        bool replay = SPEC && ctl[6] == 0;
-        if (!replay) {
 
         // ---- prologue. Keys path: the frame's Bob words staged in LDS (the
         //      product rows are free until the first check phase) and its
@@ -501,18 +494,23 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
 
         // ---- iterations (:212-330): interval iterations (qkd_spec.h) in the
         //      speculative launch, the reference's binary64 ones otherwise
-        constexpr bool spec = SPEC;
+        bool spec = SPEC && ctl[6] != 0;
+        // a frame the policy keeps off the speculation counts as replayed (so
+        // the policy, once on, stays on, and the call's count reports it)
+        if (SPEC && !spec && tid == 0) atomicAdd(a.replay_count, 1u);
         bool done = false;
         uint32_t it = 0;
         for (;;) {
             if (it >= a.max_it) break;
             const bool folded = fold1 && it == 0;
             uint32_t* rw = ctl + 4 + (rnd & 1u);
-            if constexpr (SPEC) {
-                if (!folded) {
-                    spec_check_phase<DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn, a.thr_up,
-                                         rw, wave, lane);
-                    __syncthreads();
+            if (SPEC && spec) {
+                if constexpr (SPEC) {
+                    if (!folded) {
+                        spec_check_phase<DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
+                                             a.thr_up, rw, wave, lane);
+                        __syncthreads();
+                    }
                 }
             } else if (!folded) {
                 if (TABLES && it == 1 && tab2_on)
@@ -529,18 +527,20 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
             // the hard decision's syndrome (:277, calculate_syndrome_irregular :476-486),
             // then b2c_k = clamp(total_i - c2b_k) (:303-316) into slot k.
-            if constexpr (SPEC) {
-                if (folded)
-                    spec_bit_phase<true>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
-                else
-                    spec_bit_phase<false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
+            if (SPEC && spec) {
+                if constexpr (SPEC) {
+                    if (folded)
+                        spec_bit_phase<true>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
+                    else
+                        spec_bit_phase<false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
+                }
             } else
-            for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kBitChunk) {
-                T v[kBitChunk][kDvUnroll];
-                int32_t jc[kBitChunk][kDvUnroll];
-                int dg[kBitChunk];
+            for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += BC) {
+                T v[BC][kDvUnroll];
+                int32_t jc[BC][kDvUnroll];
+                int dg[BC];
 #pragma unroll
-                for (int u = 0; u < kBitChunk; ++u) {
+                for (int u = 0; u < BC; ++u) {
                     const int i = tid + (r0 + u) * kDecodeBlock;
                     const bool ok = i < c.n;
                     dg[u] = ok ? c.bit_deg[i] : 0;
@@ -558,7 +558,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < kBitChunk; ++u) {
+                for (int u = 0; u < BC; ++u) {
                     const int r = r0 + u;
                     if (r * kDecodeBlock >= c.n) break;            // block-uniform
                     const int i = tid + r * kDecodeBlock;
@@ -663,8 +663,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // whose hard decision is the output and must then be certain too;
             // or no uncertainty at all (bit 2 clear: the decision is exact).
             if (spec && ((fl & 2u) || ((fl & 4u) && (!(fl & 1u) || it + 1 >= a.max_it)))) {
-                replay = true;          // decode the frame exactly (next launch)
-                break;
+                // decode the frame exactly
+                spec = false;
+                it = 0;
+                if (tid == 0) {
+                    atomicAdd(a.replay_count, 1u);
+                    atomicAdd(a.spec_replays, 1ull);
+                }
+                continue;
             }
 #ifndef QKD_EXP_NO_STOP
             if (!(fl & 1u)) {
@@ -674,35 +680,30 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
 #endif
             ++it;
             if (spec && it >= a.spec_cap && it < a.max_it) {
-                replay = true;
-                break;
+                spec = false;
+                it = 0;
+                if (tid == 0) {
+                    atomicAdd(a.replay_count, 1u);
+                    atomicAdd(a.spec_replays, 1ull);
+                }
             }
         }
 
         // ---- outputs: SP_result and the last hard decision (keys path:
         //      packed, for key_match_kernel's arrays_equal, :433)
-        if (!replay) {
-            if (MODE == kModeKeys) {
-                for (int q = tid; q < (int)a.words; q += kDecodeBlock) a.zout[(size_t)f * a.words + q] = zw[q];
-            } else if (a.bits_out) {
-                for (int i = tid; i < c.n; i += kDecodeBlock)
-                    a.bits_out[(size_t)f * c.n + i] = (uint8_t)((zw[i >> 6] >> (i & 63)) & 1u);
-            }
-            if (tid == 0) {
-                a.iters[f] = done ? it + 1 : a.max_it;
-                a.sp_ok[f] = done ? 1 : 0;
-            }
+        if (MODE == kModeKeys) {
+            for (int q = tid; q < (int)a.words; q += kDecodeBlock) a.zout[(size_t)f * a.words + q] = zw[q];
+        } else if (a.bits_out) {
+            for (int i = tid; i < c.n; i += kDecodeBlock)
+                a.bits_out[(size_t)f * c.n + i] = (uint8_t)((zw[i >> 6] >> (i & 63)) & 1u);
         }
-        }   // !replay on entry
         if (tid == 0) {
-            if (SPEC && replay) {
-                a.replay_list[atomicAdd(a.replay_count, 1u)] = f;
-                atomicAdd(a.spec_replays, 1ull);
-            }
+            a.iters[f] = done ? it + 1 : a.max_it;
+            a.sp_ok[f] = done ? 1 : 0;
             ctl[1] = next_f;
-            // speculate on the next frame unless a quarter of the frames
-            // started so far (past the first 64) were replayed
-            ctl[6] = launch_replays * 4u <= next_f + 64u ? 1u : 0u;
+            // speculate on the next frame unless a sixth of the frames
+            // started so far (past the first 64) were replayed (kSpecReplayMax)
+            ctl[6] = launch_replays * 6u <= next_f + 64u ? 1u : 0u;
         }
         __syncthreads();
     }

@@ -15,6 +15,9 @@ namespace qkd {
 // Speculative interval iterations per frame before the exact fallback
 // (decode_split.hip; QKD_SPEC_CAP overrides).
 constexpr int kSpecCapDefault = 8;
+// Replay fraction above which speculation stops: within a launch for the
+// frames still to start (decode_split.hip), across calls for that QBER and up.
+constexpr double kSpecReplayMax = 1.0 / 6.0;
 
 // Largest check degree the first-iteration table covers.
 constexpr int kFirstTableDeg = 16;
@@ -97,10 +100,8 @@ struct DecodeArgs {
     uint32_t spec_cap;
     float lp_dn, lp_up, thr_dn, thr_up;
     unsigned long long* spec_replays;
-    // the frames the speculative launch leaves to the exact one: the list and
-    // its length (zeroed per call); once the list passes a quarter of the
-    // frames started, the remaining frames skip the speculation
-    uint32_t* replay_list;
+    // frames replayed exactly in this launch (zeroed per launch): once they
+    // pass a quarter of the frames started, later frames skip the speculation
     uint32_t* replay_count;
 };
 
@@ -188,6 +189,7 @@ struct DecodeLds {
 // (bits tid + r*kDecodeBlock) per load batch.
 constexpr int kDvUnroll = 3;
 constexpr int kBitChunk = 5;
+constexpr int kBitChunkSpec = 2;     // the exact iterations inside the speculative kernel
 // the second-iteration table index and the first-message fold read a bit's
 // messages from the unrolled rows only
 static_assert(kTab2MaxDv <= kDvUnroll, "tables need every row of their bits unrolled");
@@ -407,7 +409,7 @@ using DecodeFn = void (*)(DecodeArgs);
 // decode_split.hip: the split-store kernel for (mode, rule in {kRuleSp64,
 // kRuleSp32}, clamp, check-degree bucket); *dc receives the bucket.
 DecodeFn pick_split_decode(int mode, int rule, bool clamp, int max_dc, int* dc);
-// The speculative launch of the QKD path (binary64 rule, clamp on).
+// The speculative kernel of the QKD path (binary64 rule, clamp on).
 DecodeFn pick_split_spec(int max_dc, int* dc);
 // decode_split.hip, kModeKeys: the kernels around the split decoder.
 // Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.

@@ -81,11 +81,20 @@ struct qkd_workspace {
     // words the decoder leaves for key_match_kernel; sized with the keys
     uint32_t* synw = nullptr;
     uint64_t* zout = nullptr;
-    uint32_t* replay = nullptr;     // frames the speculative launch leaves to the exact one
     // keygen shuffle scratch (ne words per frame)
     uint32_t* low = nullptr;
     size_t low_words = 0;
     hipEvent_t done = nullptr;
+    // speculation policy across calls (decode.hip, decode_keys): the replay
+    // count of the last speculative call comes back asynchronously; a QBER
+    // point whose frames were replayed too often turns the speculation off for
+    // it and every higher QBER on this workspace
+    uint32_t* spec_stat_host = nullptr;     // pinned: replays of the last call
+    hipEvent_t spec_stat_ev = nullptr;
+    bool spec_stat_pending = false;
+    double spec_stat_q = 0.0;
+    size_t spec_stat_frames = 0;
+    double spec_off_q = 2.0;
 };
 
 struct qkd_code {
