@@ -1101,7 +1101,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             // replays in place) when it applies: QKD path with the folded first
             // iteration, binary64 rule, clamped messages, bit degree <= kDvUnroll
             const bool spec = mode == kModeKeys && rule == kRuleSp64 && a.spec_cap > 0 && a.clamp_on &&
-                              a.first_table && c->max_dv <= kDvUnroll;
+                              a.first_table && c->max_dv <= kDvUnroll && c->d_bit_code;
             if (spec) {
                 int xdc = 0, sgrid = 0;
                 DecodeFn xfn = pick_split_spec(c->max_dc, &xdc);

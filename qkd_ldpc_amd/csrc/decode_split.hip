@@ -255,7 +255,7 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
 // the binary32 and the reference's binary64 rounding allowances, clamped with
 // med3. A hard decision whose sign the interval leaves open marks its checks
 // in xunc (the syndrome test then decides whether the round can stand).
-// Bit degree <= kDvUnroll.
+// Needs DeviceCode::bit_code (bit degree <= 3, M <= 65536, check degree <= 16).
 template <bool FOLD>
 __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const DecodeArgs& a, const SplitStore<double>& ms,
                                                const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
@@ -267,20 +267,16 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
     for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kBitChunk) {
         double v[kBitChunk][kDvUnroll];
-        int32_t jc[kBitChunk][kDvUnroll];
-        int dg[kBitChunk];
+        uint64_t bc[kBitChunk];                 // the bits' packed words (DeviceCode::bit_code)
 #pragma unroll
         for (int u = 0; u < kBitChunk; ++u) {
             const int i = tid + (r0 + u) * kDecodeBlock;
             const bool ok = i < c.n;
-            dg[u] = ok ? c.bit_deg[i] : 0;
+            bc[u] = ok ? c.bit_code[i] : 0;
             const uint32_t iw = (uint32_t)((r0 + u) * kDecodeBlock + wave * 64);
 #pragma unroll
-            for (int k = 0; k < kDvUnroll; ++k) {
-                const bool ld = ok && k < c.max_dv;
+            for (int k = 0; k < kDvUnroll; ++k)
                 v[u][k] = FOLD ? 0.0 : ms.ld_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i);
-                jc[u][k] = ld ? c.bit_chk[k * n_pad + i] : 0;
-            }
         }
 #pragma unroll
         for (int u = 0; u < kBitChunk; ++u) {
@@ -289,7 +285,10 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             const int i = tid + r * kDecodeBlock;
             const uint32_t iw = (uint32_t)(r * kDecodeBlock + wave * 64);
             const bool ok = i < c.n;
-            const int deg = dg[u];
+            const int deg = (int)(bc[u] >> 48) & 3;
+            int32_t jc[kDvUnroll];
+#pragma unroll
+            for (int k = 0; k < kDvUnroll; ++k) jc[k] = (int32_t)(bc[u] >> (16 * k)) & 0xffff;
             const uint32_t bob = (bobmask >> r) & 1u;
             bool z, unc = false;
             f2 bo[kDvUnroll];
@@ -302,9 +301,9 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 for (int k = 0; k < kDvUnroll; ++k) {
                     cv[k] = 0.0;
                     if (k < deg) {
-                        const int j = jc[u][k];
+                        const int j = jc[k];
                         const uint32_t sp = (qsyn[j >> 5] >> (j & 31)) & 1u;
-                        const double cm = ctab[c.chk_deg[j]];
+                        const double cm = ctab[((uint32_t)(bc[u] >> (50 + 4 * k)) & 15u) + 1u];
                         cv[k] = (sp ^ sgi) ? -cm : cm;
                     }
                 }
@@ -349,12 +348,12 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             if (z) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
-                    if (k < deg) atomicXor(&xsyn[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
+                    if (k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
             }
             if (unc) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
-                    if (k < deg) atomicOr(&xunc[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
+                    if (k < deg) atomicOr(&xunc[jc[k] >> 5], 1u << (jc[k] & 31));
             }
             if (!keep || !ok) continue;
 #pragma unroll

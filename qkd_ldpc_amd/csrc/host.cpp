@@ -43,6 +43,8 @@ static void free_device(qkd_code* c) {
     c->d_bit_pos = nullptr;
     if (c->d_bit_deg) (void)hipFree(c->d_bit_deg);
     if (c->d_bit_pat) (void)hipFree(c->d_bit_pat);
+    if (c->d_bit_code) (void)hipFree(c->d_bit_code);
+    c->d_bit_code = nullptr;
     if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
     c->d_bit_pat = nullptr;
     c->d_pat_deg = nullptr;
@@ -192,6 +194,23 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         QKD_HIP(hipMemcpy(c->d_bit_pat, bit_pat.data(), bit_pat.size() * sizeof(uint16_t),
                           hipMemcpyHostToDevice));
         QKD_HIP(hipMemcpy(c->d_pat_deg, c->pat_deg.data(), c->pat_deg.size(), hipMemcpyHostToDevice));
+    }
+    // packed per-bit words for the speculative bit phases (qkd_internal.h)
+    bool packable = m <= 65536 && max_dv <= 3;
+    for (int32_t j = 0; j < m && packable; ++j) packable = chk_deg[j] >= 1 && chk_deg[j] <= 16;
+    if (packable) {
+        std::vector<uint64_t> code((size_t)c->n_pad, 0);
+        for (int32_t i = 0; i < n; ++i) {
+            uint64_t w = (uint64_t)bdeg[i] << 48;
+            for (int32_t k = 0; k < bdeg[i]; ++k) {
+                const int32_t j = bit_chk[(size_t)k * c->n_pad + i];
+                w |= (uint64_t)j << (16 * k);
+                w |= (uint64_t)(chk_deg[j] - 1) << (50 + 4 * k);
+            }
+            code[i] = w;
+        }
+        QKD_HIP(hipMalloc(&c->d_bit_code, code.size() * sizeof(uint64_t)));
+        QKD_HIP(hipMemcpy(c->d_bit_code, code.data(), code.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
     }
     std::vector<uint2> plan2(plan.word.size());
     for (size_t k = 0; k < plan.word.size(); ++k) plan2[k] = make_uint2(plan.word[k], plan.seg[k]);

@@ -59,6 +59,11 @@ struct DeviceCode {
     int32_t n_pat;
     const uint16_t* bit_pat;
     const uint8_t* pat_deg;
+    // packed per-bit word (speculative bit phases; nullptr unless M <= 65536,
+    // bit degree <= 3 and check degree <= 16): bits 0-15 / 16-31 / 32-47 the
+    // bit's checks in ascending order (0 past its degree), 48-49 its degree,
+    // 50-53 / 54-57 / 58-61 each check's degree - 1
+    const uint64_t* bit_code;
 };
 
 }  // namespace qkd
@@ -113,6 +118,7 @@ struct qkd_code {
     int32_t n_pat = 0;                  // 0: too many degree patterns for the table
     std::vector<uint8_t> pat_deg;
     uint16_t* d_bit_pat = nullptr;
+    uint64_t* d_bit_code = nullptr;
     uint8_t* d_pat_deg = nullptr;
     // parallel key generation (decode.hip: keygen_fast_kernel): lane l of a
     // frame's wave starts at draw l * keygen_chunk; d_jump[b] = T^(chunk * 2^b)
@@ -124,7 +130,7 @@ struct qkd_code {
     qkd::DeviceCode view() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
-                               n_pat, d_bit_pat, d_pat_deg};
+                               n_pat, d_bit_pat, d_pat_deg, d_bit_code};
     }
 };
 
