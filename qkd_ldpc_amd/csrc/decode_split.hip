@@ -115,7 +115,8 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
     int t = wave;
     if (t >= n_tasks) return;
     const uint2* pl = plan + lane;
-    auto slot = [&](uint2 p) -> uint32_t { return pw_row(p) * n_pad + pw_bit(p); };
+    // n_pad < 2^24 and rows < 32: a 24-bit multiply
+    auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
     auto sbit = [&](uint2 p) -> uint32_t {
         const uint32_t j = pw_chk(p);
         return (tsyn[j >> 5] >> (j & 31)) & 1u;
@@ -182,7 +183,8 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
     // the row's DC entries past lane 63 are read (times 0) by segments ending
     // there: keep them finite (the prologue stages key words in this region)
     if (lane < DC) row[64 + lane] = 0.0;
-    auto slot = [&](uint2 p) -> uint32_t { return pw_row(p) * n_pad + pw_bit(p); };
+    // n_pad < 2^24 and rows < 32: a 24-bit multiply
+    auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
     auto edge = [&](double xv, uint2 w) -> double {
         const f2 bv = qkds::unpack_iv(xv);
         const bool neg = bv.y < 0.0f;
@@ -217,7 +219,8 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
         m.y = __builtin_fminf(m.y, thr_up);
         const uint32_t j = pw_chk(w);
         const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
-        const uint32_t sigma = sj ^ (uint32_t)seg_parity(sgn, w) ^ (neg ? 1u : 0u);
+        const uint32_t sigma =
+            sj ^ (uint32_t)(DC <= 32 ? seg_parity32(sgn, w) : seg_parity(sgn, w)) ^ (neg ? 1u : 0u);
         return qkds::pack_iv(sigma ? -m.yx : m);
     };
     uint2 wa = pl[t * 64];

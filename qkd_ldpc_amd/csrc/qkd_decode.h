@@ -205,9 +205,18 @@ __device__ __forceinline__ int pw_start(uint2 p) { return (int)((p.y >> 20) & 63
 __device__ __forceinline__ int pw_deg(uint2 p) { return (int)(p.y >> 26) + 1; }
 // Parity of the lanes of this lane's check (its segment) in a wave ballot.
 __device__ __forceinline__ int seg_parity(uint64_t ballot, uint2 w) {
+    // the segment's bits start at lane pw_start: shift them down, keep deg
+    // (<= 64) of them, count
+    const uint64_t sh = ballot >> pw_start(w);
     const int deg = pw_deg(w);
+    if (deg <= 32) return __popc(__builtin_amdgcn_ubfe((uint32_t)sh, 0, (uint32_t)deg)) & 1;
     const uint64_t m = deg == 64 ? ~0ull : ((1ull << deg) - 1ull);
-    return __popcll(ballot & (m << pw_start(w))) & 1;
+    return __popcll(sh & m) & 1;
+}
+// The same for segments known to be at most 32 lanes long.
+__device__ __forceinline__ int seg_parity32(uint64_t ballot, uint2 w) {
+    const uint32_t sh = (uint32_t)(ballot >> pw_start(w));
+    return __popc(__builtin_amdgcn_ubfe(sh, 0, (uint32_t)pw_deg(w))) & 1;
 }
 
 // One edge of the check phase (qkd_ldpc_algorithm.cpp:220-249):
