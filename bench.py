@@ -72,10 +72,10 @@ def pmc_traffic():
     tools/pmc_traffic.py (separate rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_decode*.json")))
     if not files:
-        return None, None
+        return None, None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT), d.get("valu_busy")
 
 
 def measure_variants(args, step, stream, counters, iters, Q, F, q, steps=5):
@@ -174,6 +174,7 @@ def main():
         if world > 1:
             allreduce_counters(counters)
 
+    Q.spec_replays(ws, reset=True)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -205,7 +206,8 @@ def main():
     alg_bytes = sum_it_local * b_iter + F * B_FRAME
     avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9
-    traffic, traffic_src = pmc_traffic()
+    traffic, traffic_src, valu_busy = pmc_traffic()
+    replays = Q.spec_replays(ws, reset=True)
 
     stats = Q.counters_to_stats(c, frames_total, args.max_iters, q)
     if rank == 0:
@@ -241,10 +243,18 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "decode_kernel (qkd_qkd_ldpc_batch, HIP events on its stream)",
+                "kernel": "qkd_qkd_ldpc_batch = pack + frame_syn_kernel + decode_split_kernel (speculative) "
+                          "+ key_match_kernel, HIP events on its stream",
                 "kernel_ms": avg_kernel_s * 1e3,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "traffic_source": traffic_src,
+                "valu_busy_pmc": valu_busy,
+            },
+            "speculation": {
+                "replayed_frames": replays,
+                "frames": F * (args.steps + args.warmup),
+                "note": "frames whose interval iterations could not certify every hard "
+                        "decision, decoded again exactly (outputs bit-exact either way)",
             },
         }
         if os.environ.get("QKD_PHASE_TIMING"):

@@ -39,6 +39,7 @@ __all__ = [
     "sum_product_decoding_irregular", "sum_product_decoding_regular", "qkd_ldpc",
     "QKD_LDPC_irregular", "QKD_LDPC_regular", "keygen", "run_trials", "make_seeds",
     "qber_range", "Workspace", "counters_to_stats", "decoder_flags", "trace_decode",
+    "spec_replays",
 ]
 
 
@@ -187,6 +188,15 @@ class Workspace:
 
 def _ws(ws):
     return ws.handle if ws is not None else None
+
+
+def spec_replays(ws: Workspace, reset: bool = False) -> int:
+    """Frames of the QKD path decoded on `ws` whose speculative interval
+    iterations could not certify every hard decision and were decoded again
+    exactly (qkd_debug_spec_replays); outputs never depend on it."""
+    v = C.c_uint64(0)
+    N.check(N.lib().qkd_debug_spec_replays(ws.handle, C.byref(v), int(reset)))
+    return int(v.value)
 
 
 def calculate_syndrome(H: HMatrix, bits, stream=None):
