@@ -45,7 +45,8 @@ constexpr float kPhiHugeHi = 4.0e-35f;
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // [lo, hi]; packed binary32 ops
 
-// phi(x) and |phi'(x)| = 1 / sinh(x) for finite x > 0 (x >= kPhiHuge: 0, 0).
+// phi(x) and an upper bound of |phi'(x)| = 1 / sinh(x) (within a factor 2)
+// for finite x > 0 (x >= kPhiHuge: 0, 0).
 struct PhiVal {
     float v;
     float slope;
@@ -73,10 +74,12 @@ __device__ __forceinline__ PhiVal phi_eval(float x) {
     t = __builtin_fmaf(x, t, 1.0f);
     const float w = x < 0.35f ? x * t : 1.0f - u;
     const float w2 = 2.0f - w;
-    // x < 1: phi = ln((2 - w) / w) = ln 2 (log2(2 - w) - log2(w)); the
-    // difference is >= 1.1 (v_log_f32 is accurate to ~2^-22 absolute near 1,
-    // so the logs are kept away from small results)
-    const float vlo = 0.693147180559945f * (__builtin_amdgcn_logf(w2) - __builtin_amdgcn_logf(w));
+    const float rw = __builtin_amdgcn_rcpf(w);
+    // x < 1: phi = ln((2 - w) / w) = ln 2 log2((2 - w) * rcp(w)); the
+    // argument is >= 2.16 (v_log_f32 is accurate to ~2^-22 absolute near 1,
+    // so the log is kept away from small results; rcp and the product add
+    // 1.5 ulp of the argument)
+    const float vlo = 0.693147180559945f * __builtin_amdgcn_logf(w2 * rw);
     // x >= 1: phi = 2 atanh(u) = 2u (1 + s/3 + s^2/5 + ... + s^8/17), s = u^2 <= e^-2
     // (truncation < s^9 / 19 < 1e-9 relative)
     const float s = u * u;
@@ -91,8 +94,9 @@ __device__ __forceinline__ PhiVal phi_eval(float x) {
     const float vhi = (2.0f * u) * h;
     PhiVal o;
     o.v = x < 1.0f ? vlo : vhi;
-    // 1 / sinh(x) = 2u / (1 - u^2) = 2u / (w (2 - w))
-    o.slope = (2.0f * u) * __builtin_amdgcn_rcpf(w * w2);
+    // |phi'(x)| = 1 / sinh(x) = 2u / (w (2 - w)) <= 2u / w (2 - w >= 1): an
+    // upper bound within a factor 2, which is all the tangent below needs
+    o.slope = (2.0f * u) * rw;
     if (!(x < kPhiHuge)) {
         o.v = 0.0f;
         o.slope = 0.0f;
