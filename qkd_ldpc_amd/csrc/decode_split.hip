@@ -414,6 +414,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     if (tid == 0) { ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
     static_assert(!SPEC || (TABLES && CLAMP), "speculation: QKD path, binary64 rule, clamped messages");
     constexpr int BC = SPEC ? kBitChunkSpec : kBitChunk;      // exact bit phase load batch
+#ifdef QKD_EXP_NO_REPLAY
+    constexpr bool EXACT_IN = !SPEC;     // diagnostic: the speculative kernel without its exact path
+#else
+    constexpr bool EXACT_IN = true;
+#endif
     if (TABLES && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
     if (tab2_on) {
         __syncthreads();
@@ -514,7 +519,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                         __syncthreads();
                     }
                 }
-            } else if (!folded) {
+            } else if (EXACT_IN && !folded) {
                 if (TABLES && it == 1 && tab2_on)
                     split_check_phase<kSrcTable, CLAMP, DC, RULE>(c.plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);
@@ -536,7 +541,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     else
                         spec_bit_phase<false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
                 }
-            } else
+            } else if (EXACT_IN)
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += BC) {
                 T v[BC][kDvUnroll];
                 int32_t jc[BC][kDvUnroll];
