@@ -259,6 +259,10 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
 // med3. A hard decision whose sign the interval leaves open marks its checks
 // in xunc (the syndrome test then decides whether the round can stand).
 // Needs DeviceCode::bit_code (bit degree <= 3, M <= 65536, check degree <= 16).
+#ifndef QKD_IV_CHUNK
+#define QKD_IV_CHUNK 3
+#endif
+constexpr int kIvChunk = QKD_IV_CHUNK;       // rounds per load batch
 template <bool FOLD>
 __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const DecodeArgs& a, const SplitStore<double>& ms,
                                                const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
@@ -268,11 +272,11 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
     const uint32_t n_pad = (uint32_t)c.n_pad;
     const double llr_p = a.log_p;
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
-    for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kBitChunk) {
-        double v[kBitChunk][kDvUnroll];
-        uint64_t bc[kBitChunk];                 // the bits' packed words (DeviceCode::bit_code)
+    for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kIvChunk) {
+        double v[kIvChunk][kDvUnroll];
+        uint64_t bc[kIvChunk];                 // the bits' packed words (DeviceCode::bit_code)
 #pragma unroll
-        for (int u = 0; u < kBitChunk; ++u) {
+        for (int u = 0; u < kIvChunk; ++u) {
             const int i = tid + (r0 + u) * kDecodeBlock;
             const bool ok = i < c.n;
             bc[u] = ok ? c.bit_code[i] : 0;
@@ -282,7 +286,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 v[u][k] = FOLD ? 0.0 : ms.ld_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i);
         }
 #pragma unroll
-        for (int u = 0; u < kBitChunk; ++u) {
+        for (int u = 0; u < kIvChunk; ++u) {
             const int r = r0 + u;
             if (r * kDecodeBlock >= c.n) break;            // block-uniform
             const int i = tid + r * kDecodeBlock;
