@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--max-iters", type=int, default=50)
     ap.add_argument("--threshold", type=float, default=100.0)
     ap.add_argument("--seed", type=int, default=777)
-    ap.add_argument("--cpu-frames", type=int, default=4096,
+    ap.add_argument("--cpu-frames", type=int, default=8192,
                     help="frames in the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
