@@ -1091,20 +1091,21 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 QKD_HIP(hipMemsetAsync(a.phase, 0, 64, stream));
             }
             a.replay_count = ws->counter + 1;
+            a.spec_replays = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 120);
             if (mode == kModeKeys) {
                 a.synw = ws->synw;
                 a.zout = ws->zout;
-                a.spec_replays = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 120);
                 QKD_HIP(launch_frame_syn(a, stream));
             }
             // the speculative kernel (interval iterations, qkd_spec.h, exact
             // replays in place) when it applies: QKD path with the folded first
             // iteration, binary64 rule, clamped messages, bit degree <= kDvUnroll
-            const bool spec = mode == kModeKeys && rule == kRuleSp64 && a.spec_cap > 0 && a.clamp_on &&
-                              a.first_table && c->max_dv <= kDvUnroll && c->d_bit_code;
+            // (the QKD path needs its folded first iteration; the LLR path starts from the LLRs)
+            const bool spec = rule == kRuleSp64 && a.spec_cap > 0 && a.clamp_on &&
+                              (mode == kModeLlr || a.first_table) && c->max_dv <= kDvUnroll && c->d_bit_code;
             if (spec) {
                 int xdc = 0, sgrid = 0;
-                DecodeFn xfn = pick_split_spec(c->max_dc, &xdc);
+                DecodeFn xfn = pick_split_spec(mode, c->max_dc, &xdc);
                 s = decode_grid(c, xfn, L.bytes, &sgrid);
                 if (s != QKD_OK) return s;
                 sfn = xfn;
@@ -1212,6 +1213,14 @@ qkd_status qkd_syndrome_batch(const qkd_code* c, const uint8_t* bits, size_t n_f
     return QKD_OK;
 }
 
+// binary32 bound of a binary64 value: the largest float <= x (up: smallest >= x)
+static float f32_bound(double x, bool up) {
+    float f = (float)x;
+    if (up && (double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    if (!up && (double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+}
+
 qkd_status qkd_decode_batch(const qkd_code* c, qkd_workspace* ws, const double* llr,
                             const uint8_t* syndrome, size_t n_frames, uint32_t max_iterations,
                             double msg_threshold, uint32_t flags, uint8_t* bits_out,
@@ -1236,16 +1245,16 @@ qkd_status qkd_decode_batch(const qkd_code* c, qkd_workspace* ws, const double* 
     a.bits_out = bits_out;
     a.iters = iterations;
     a.sp_ok = syndromes_match;
+    // speculative interval iterations (decode_split.hip, qkd_spec.h): binary64
+    // rule with clamped messages; QKD_SPEC_CAP overrides how many (0: off)
+    int cap = kSpecCapDefault;
+    if (const char* e = getenv("QKD_SPEC_CAP")) cap = std::max(0, atoi(e));
+    a.spec_cap = (rule_of(flags) == kRuleSp64 && a.clamp_on) ? (uint32_t)cap : 0u;
+    a.thr_dn = f32_bound(msg_threshold, false);
+    a.thr_up = f32_bound(msg_threshold, true);
     return launch_decode(c, ws, a, kModeLlr, flags, (hipStream_t)stream);
 }
 
-// binary32 bound of a binary64 value: the largest float <= x (up: smallest >= x)
-static float f32_bound(double x, bool up) {
-    float f = (float)x;
-    if (up && (double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
-    if (!up && (double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
-    return f;
-}
 
 // Shared by qkd_qkd_ldpc_batch and qkd_trials_batch: keys already packed in ws.
 static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_frames, double q,

@@ -263,11 +263,11 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
 #define QKD_IV_CHUNK 3
 #endif
 constexpr int kIvChunk = QKD_IV_CHUNK;       // rounds per load batch
-template <bool FOLD>
+template <bool FOLD, int MODE>
 __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const DecodeArgs& a, const SplitStore<double>& ms,
                                                const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
                                                uint32_t* xunc, uint64_t* zw, uint32_t bobmask, bool keep,
-                                               int tid, int wave, int lane) {
+                                               uint32_t f, int tid, int wave, int lane) {
     using qkds::f2;
     const uint32_t n_pad = (uint32_t)c.n_pad;
     const double llr_p = a.log_p;
@@ -320,10 +320,12 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) bo[k] = qkds::iv_of(clamp_msg(acc - cv[k], a.thr));
             } else {
-                const f2 L = bob ? f2{-a.lp_up, -a.lp_dn} : f2{a.lp_dn, a.lp_up};
+                f2 L;
+                if constexpr (MODE == kModeLlr) L = qkds::iv_of(ok ? a.llr[(size_t)f * c.n + i] : 0.0);
+                else L = bob ? f2{-a.lp_up, -a.lp_dn} : f2{a.lp_dn, a.lp_up};
                 f2 cs[kDvUnroll];
                 f2 T = L;
-                float mag = a.lp_up;
+                float mag = __builtin_fmaxf(__builtin_fabsf(L.x), __builtin_fabsf(L.y));
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) {
                     cs[k] = k < deg ? qkds::unpack_iv(v[u][k]) : f2{0.0f, 0.0f};
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     const bool tab2_on = fold1 && a.tab2_entries;
     uint32_t rnd = 0;    // rounds (iterations of any frame) run by this workgroup
     if (tid == 0) { ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
-    static_assert(!SPEC || (TABLES && CLAMP), "speculation: QKD path, binary64 rule, clamped messages");
+    static_assert(!SPEC || (RULE == kRuleSp64 && CLAMP), "speculation: binary64 rule, clamped messages");
     constexpr int BC = SPEC ? kBitChunkSpec : kBitChunk;      // exact bit phase load batch
 #ifdef QKD_EXP_NO_REPLAY
     constexpr bool EXACT_IN = !SPEC;     // diagnostic: the speculative kernel without its exact path
@@ -467,8 +469,12 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
         // Bob's bits of this thread's bit-phase rounds (round r: bit tid + r *
         // kDecodeBlock; N <= 32 * kDecodeBlock, kMaxBitsLds). Without the fold
         // the first check phase reads b2c = LLR_i (:188) from every slot.
+        // (the speculative kernel's replay policy for this frame: ctl[6])
+        const bool spec0 = SPEC && ctl[6] != 0;
         uint32_t bobmask = 0;
-        {
+        // the first check phase's b2c = LLR_i in every slot (:188), as enclosing
+        // intervals when speculating (the LLR path has no folded first iteration)
+        auto init_slots = [&](bool as_interval) {
             int r = 0;
             for (int i = tid; i < c.n; i += kDecodeBlock, ++r) {
                 T l;
@@ -480,14 +486,17 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     l = bb ? -llr_p : llr_p;
                 }
                 if (!fold1) {
+                    T sv = l;
+                    if constexpr (SPEC) if (as_interval) sv = qkds::pack_iv(qkds::iv_of((double)l));
                     const int deg = c.bit_deg[i];
-                    for (int k = 0; k < deg; ++k) ms.st((uint32_t)k * n_pad + i, l);
+                    for (int k = 0; k < deg; ++k) ms.st((uint32_t)k * n_pad + i, sv);
                 }
             }
             // the dummy column's slot (idle plan lanes): a finite value, and
             // table index 0 for the second check phase
             if (tid == 0) ms.st((uint32_t)c.n, (T)0);
-        }
+        };
+        init_slots(spec0);
         // ---- prologue, LLR path: target syndrome bits per check (tsyn), thread per check
         if (MODE == kModeLlr) {
             for (int j0 = wave * 64; j0 < c.m; j0 += kDecodeBlock) {
@@ -505,7 +514,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
 
         // ---- iterations (:212-330): interval iterations (qkd_spec.h) in the
         //      speculative launch, the reference's binary64 ones otherwise
-        bool spec = SPEC && ctl[6] != 0;
+        bool spec = spec0;
         // a frame the policy keeps off the speculation counts as replayed (so
         // the policy, once on, stays on, and the call's count reports it)
         if (SPEC && !spec && tid == 0) atomicAdd(a.replay_count, 1u);
@@ -541,9 +550,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             if (SPEC && spec) {
                 if constexpr (SPEC) {
                     if (folded)
-                        spec_bit_phase<true>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
+                        spec_bit_phase<true, MODE>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, f, tid,
+                                                   wave, lane);
                     else
-                        spec_bit_phase<false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, tid, wave, lane);
+                        spec_bit_phase<false, MODE>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, f, tid,
+                                                    wave, lane);
                 }
             } else if (EXACT_IN)
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += BC) {
@@ -677,6 +688,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                 // decode the frame exactly
                 spec = false;
                 it = 0;
+                if (!fold1) {           // the LLR path starts from LLR_i in every slot again
+                    init_slots(false);
+                    __syncthreads();
+                }
                 if (tid == 0) {
                     atomicAdd(a.replay_count, 1u);
                     atomicAdd(a.spec_replays, 1ull);
@@ -693,6 +708,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             if (spec && it >= a.spec_cap && it < a.max_it) {
                 spec = false;
                 it = 0;
+                if (!fold1) {
+                    init_slots(false);
+                    __syncthreads();
+                }
                 if (tid == 0) {
                     atomicAdd(a.replay_count, 1u);
                     atomicAdd(a.spec_replays, 1ull);
@@ -835,7 +854,10 @@ static DecodeFn pick_split_dc(int max_dc, int* dc) {
     return decode_split_kernel<MODE, RULE, 64, CLAMP, SPEC>;
 }
 
-DecodeFn pick_split_spec(int max_dc, int* dc) { return pick_split_dc<kModeKeys, kRuleSp64, true, true>(max_dc, dc); }
+DecodeFn pick_split_spec(int mode, int max_dc, int* dc) {
+    return mode == kModeLlr ? pick_split_dc<kModeLlr, kRuleSp64, true, true>(max_dc, dc)
+                            : pick_split_dc<kModeKeys, kRuleSp64, true, true>(max_dc, dc);
+}
 
 template <int MODE, int RULE>
 static DecodeFn pick_split_clamp(bool clamp, int max_dc, int* dc) {

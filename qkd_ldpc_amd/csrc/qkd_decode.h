@@ -418,8 +418,8 @@ using DecodeFn = void (*)(DecodeArgs);
 // decode_split.hip: the split-store kernel for (mode, rule in {kRuleSp64,
 // kRuleSp32}, clamp, check-degree bucket); *dc receives the bucket.
 DecodeFn pick_split_decode(int mode, int rule, bool clamp, int max_dc, int* dc);
-// The speculative kernel of the QKD path (binary64 rule, clamp on).
-DecodeFn pick_split_spec(int max_dc, int* dc);
+// The speculative kernel (binary64 rule, clamp on) for a mode.
+DecodeFn pick_split_spec(int mode, int max_dc, int* dc);
 // decode_split.hip, kModeKeys: the kernels around the split decoder.
 // Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.
 hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream);

@@ -156,3 +156,34 @@ def test_spec_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, thr):
         assert its[k] == want["iters"], (q, thr, k)
         assert bool(sp[k]) == want["sp_ok"] and bool(ko[k]) == want["key_ok"]
         assert (bits[k] == want["out"]).all(), (q, thr, k)
+
+
+@pytest.mark.parametrize("cap", ["0", "8"])
+@pytest.mark.parametrize("q", [0.02, 0.05])
+def test_spec_llr_path_matches_oracle(Q, H, oracle_code, monkeypatch, cap, q):
+    """qkd_decode_batch (the reference's sum_product_decoding, LLR input) with
+    the speculation on and off: decoded words, iteration counts and flags equal
+    the oracle's; the LLR path has no folded first iteration, so the intervals
+    start from the LLRs themselves."""
+    monkeypatch.setenv("QKD_SPEC_CAP", cap)
+    rng = np.random.default_rng(int(q * 1000))
+    f = 24
+    alice = rng.integers(0, 2, (f, 10240))
+    bob = alice ^ (rng.random((f, 10240)) < q)
+    lp = np.log((1 - q) / q)
+    llr = np.where(bob == 1, -lp, lp) * (1.0 + 0.25 * rng.random((f, 10240)))   # not +-log_p only
+    syn = np.stack([oracle_code.syndrome(a) for a in alice]).astype(np.uint8)
+    ws = Q.Workspace(H)
+    Q.spec_replays(ws, reset=True)
+    r = Q.sum_product_decoding(H, torch.from_numpy(llr).cuda(), torch.from_numpy(syn).cuda(), 50, 100.0, True,
+                               workspace=ws)
+    torch.cuda.synchronize()
+    bits = r.bits.cpu().numpy()
+    its = r.iterations.cpu().numpy()
+    ok = r.syndromes_match.cpu().numpy()
+    for k in range(f):
+        want = oracle_code.decode(llr[k], syn[k], 50, 100.0, True)
+        assert its[k] == want["iters"], (cap, q, k)
+        assert bool(ok[k]) == want["sp_ok"]
+        assert (bits[k] == want["out"]).all(), (cap, q, k)
+    print(f"LLR path cap {cap} q {q}: {Q.spec_replays(ws)} of {f} replayed")
