@@ -747,19 +747,25 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
 // first-iteration product, q_j = s_j ^ (H * bob)_j ^ (deg_j & sign(log_p))
 // (first_check_phase), one bit per check in whole 64-check groups. kSynFrames
 // frames per workgroup share each load of a check's row.
-constexpr int kSynFrames = 8;
+constexpr int kSynFrames = 4;
 constexpr int kSynBlock = 256;
+constexpr int kSynRow = 8;
 __global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, const uint64_t* __restrict__ alice_w,
                                                               const uint64_t* __restrict__ bob_w, uint32_t words,
                                                               uint32_t n_frames, uint32_t lsign, uint32_t* synw) {
-    extern __shared__ uint64_t kw[];   // [kSynFrames][alice | bob][words]
+    // [kSynFrames][2 * words] pairs (Alice's 32-bit word, Bob's 32-bit word):
+    // one 8-byte LDS read gives both keys' bit
+    extern __shared__ uint2 kw[];
+    const uint32_t w32 = 2 * words;
     const uint32_t f0 = blockIdx.x * kSynFrames;
     const uint32_t nf = min((uint32_t)kSynFrames, n_frames - f0);
     for (uint32_t q = threadIdx.x; q < nf * words; q += kSynBlock) {
         const uint32_t fr = q / words;
         const uint32_t w = q - fr * words;
-        kw[(2 * fr) * words + w] = alice_w[(size_t)(f0 + fr) * words + w];
-        kw[(2 * fr + 1) * words + w] = bob_w[(size_t)(f0 + fr) * words + w];
+        const uint64_t av = alice_w[(size_t)(f0 + fr) * words + w];
+        const uint64_t bv = bob_w[(size_t)(f0 + fr) * words + w];
+        kw[fr * w32 + 2 * w] = make_uint2((uint32_t)av, (uint32_t)bv);
+        kw[fr * w32 + 2 * w + 1] = make_uint2((uint32_t)(av >> 32), (uint32_t)(bv >> 32));
     }
     __syncthreads();
     const int m_words = decode_m_words(c.m);
@@ -770,18 +776,26 @@ __global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, cons
 #pragma unroll
         for (int fr = 0; fr < kSynFrames; ++fr) pa[fr] = pb[fr] = 0;
         uint32_t deg = 0;
-        if (j < c.m) {
-            for (int k = 0; k < c.max_dc; ++k) {
-                const int bit = c.chk_bits[k * c.m_pad + j];
-                if (bit < 0) continue;
-                deg++;
-                const uint32_t wi = (uint32_t)bit >> 6, sh = (uint32_t)bit & 63u;
+        auto take = [&](int bit) {
+            if (bit < 0) return;
+            deg++;
+            const uint32_t wi = (uint32_t)bit >> 5, sh = (uint32_t)bit & 31u;
 #pragma unroll
-                for (int fr = 0; fr < kSynFrames; ++fr) {
-                    pa[fr] ^= (uint32_t)(kw[(2 * fr) * words + wi] >> sh);
-                    pb[fr] ^= (uint32_t)(kw[(2 * fr + 1) * words + wi] >> sh);
-                }
+            for (int fr = 0; fr < kSynFrames; ++fr) {
+                const uint2 v = kw[fr * w32 + wi];
+                pa[fr] ^= v.x >> sh;
+                pb[fr] ^= v.y >> sh;
             }
+        };
+        if (j < c.m) {
+            // the row's first kSynRow entries loaded together (their latencies
+            // overlap), the rest one by one
+            int bits[kSynRow];
+#pragma unroll
+            for (int k = 0; k < kSynRow; ++k) bits[k] = k < c.max_dc ? c.chk_bits[k * c.m_pad + j] : -1;
+#pragma unroll
+            for (int k = 0; k < kSynRow; ++k) take(bits[k]);
+            for (int k = kSynRow; k < c.max_dc; ++k) take(c.chk_bits[k * c.m_pad + j]);
         }
 #pragma unroll
         for (int fr = 0; fr < kSynFrames; ++fr) {
