@@ -419,7 +419,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     uint32_t rnd = 0;    // rounds (iterations of any frame) run by this workgroup
     if (tid == 0) { ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
     static_assert(!SPEC || (RULE == kRuleSp64 && CLAMP), "speculation: binary64 rule, clamped messages");
-    constexpr int BC = SPEC ? kBitChunkSpec : kBitChunk;      // exact bit phase load batch
+#ifndef QKD_EXACT_CHUNK
+#define QKD_EXACT_CHUNK kBitChunk
+#endif
+    constexpr int BC = SPEC ? kBitChunkSpec : QKD_EXACT_CHUNK;      // exact bit phase load batch
 #ifdef QKD_EXP_NO_REPLAY
     constexpr bool EXACT_IN = !SPEC;     // diagnostic: the speculative kernel without its exact path
 #else
