@@ -187,3 +187,25 @@ def test_spec_llr_path_matches_oracle(Q, H, oracle_code, monkeypatch, cap, q):
         assert bool(ok[k]) == want["sp_ok"]
         assert (bits[k] == want["out"]).all(), (cap, q, k)
     print(f"LLR path cap {cap} q {q}: {Q.spec_replays(ws)} of {f} replayed")
+
+
+def test_spec_policy_turns_off_at_high_qber(Q, H, golden_vectors, monkeypatch):
+    """At QBER 0.08 most frames cannot be certified: the first call replays
+    many (the in-launch policy stops speculating after a sixth), later calls on
+    the workspace skip the speculation for that QBER and up; the results are
+    the golden ones throughout."""
+    monkeypatch.setenv("QKD_SPEC_CAP", "8")
+    seeds = seeds_dev(Q.make_seeds(777, 10000))
+    grid = golden_vectors["c3_qnom"]
+    s = int(np.argmin(np.abs(grid - 0.08)))
+    ws = Q.Workspace(H)
+    counts = []
+    for _ in range(3):
+        Q.spec_replays(ws, reset=True)
+        r = Q.run_trials(H, seeds, float(grid[s]), s, 50, 100.0, True, workspace=ws)
+        torch.cuda.synchronize()
+        assert (r.iterations.cpu().numpy() == golden_vectors["c3_iters"][s]).all()
+        assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c3_ko"][s]).all()
+        counts.append(Q.spec_replays(ws))
+    print("replays per call at QBER 0.08:", counts)
+    assert counts[0] > 0 and counts[-1] == 0
