@@ -1010,6 +1010,7 @@ static qkd_status ws_free(qkd_workspace* ws) {
     if (ws->synw) (void)hipFree(ws->synw);
     if (ws->zout) (void)hipFree(ws->zout);
     if (ws->low) (void)hipFree(ws->low);
+    if (ws->ckpt) (void)hipFree(ws->ckpt);
     if (ws->spec_stat_ev) (void)hipEventSynchronize(ws->spec_stat_ev);
     if (ws->spec_stat_host) (void)hipHostFree(ws->spec_stat_host);
     if (ws->spec_stat_ev) (void)hipEventDestroy(ws->spec_stat_ev);
@@ -1105,11 +1106,27 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                               (mode == kModeLlr || a.first_table) && c->max_dv <= kDvUnroll && c->d_bit_code;
             if (spec) {
                 int xdc = 0, sgrid = 0;
-                DecodeFn xfn = pick_split_spec(mode, c->max_dc, &xdc);
+                const bool ckpt = mode == kModeKeys && a.ckpt_unsat > 0;
+                DecodeFn xfn = pick_split_spec(mode, c->max_dc, ckpt, &xdc);
                 s = decode_grid(c, xfn, L.bytes, &sgrid);
                 if (s != QKD_OK) return s;
                 sfn = xfn;
                 grid = std::min(sgrid, grid);
+                if (ckpt) {
+                    // one saved message store per resident workgroup
+                    const size_t need = (size_t)grid * slots;
+                    if (ws->ckpt_slots < need) {
+                        if (ws->ckpt) QKD_HIP(hipFree(ws->ckpt));
+                        ws->ckpt = nullptr;
+                        ws->ckpt_slots = 0;
+                        if (hipMalloc(&ws->ckpt, need * sizeof(double)) != hipSuccess)
+                            return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate %zu B of checkpoints",
+                                             need * sizeof(double));
+                        ws->ckpt_slots = need;
+                    }
+                    a.ckpt = ws->ckpt;
+                    a.ckpt_stride = (uint32_t)slots;
+                }
             }
             hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
             QKD_HIP(hipGetLastError());
@@ -1298,16 +1315,28 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     a.sp_ok = sp_ok;
     a.key_ok = key_ok;
     // across calls: the last speculative call's replay fraction, once its
-    // count is back (never waits); above kSpecReplayMax the speculation stays
-    // off from that QBER up
+    // count is back (never waits); above kSpecCkptSwitch the frames speculate
+    // from a checkpoint instead, from that QBER up
     if (ws->spec_stat_pending && hipEventQuery(ws->spec_stat_ev) == hipSuccess) {
         ws->spec_stat_pending = false;
-        if ((double)*ws->spec_stat_host > kSpecReplayMax * (double)ws->spec_stat_frames)
-            ws->spec_off_q = std::min(ws->spec_off_q, ws->spec_stat_q);
+        if ((double)*ws->spec_stat_host > kSpecCkptSwitch * (double)ws->spec_stat_frames)
+            ws->spec_ckpt_q = std::min(ws->spec_ckpt_q, ws->spec_stat_q);
     }
-    if (q >= ws->spec_off_q) a.spec_cap = 0;
+    // at and above that QBER: the checkpointed speculation (QKD_CKPT_UNSAT
+    // overrides its trigger; 0: exact iterations only)
+    a.ckpt = nullptr;
+    a.ckpt_stride = 0;
+    a.ckpt_unsat = 0;
+    // (QKD_SPEC_CKPT=1: the checkpointed variant at every QBER; tests)
+    const char* force_ck = getenv("QKD_SPEC_CKPT");
+    if (q >= ws->spec_ckpt_q || (force_ck && atoi(force_ck) == 1)) {
+        int cu = kCkptUnsatDefault;
+        if (const char* e = getenv("QKD_CKPT_UNSAT")) cu = std::max(0, atoi(e));
+        a.ckpt_unsat = (uint32_t)cu;
+        if (cu == 0) a.spec_cap = 0;
+    }
     qkd_status st = launch_decode(c, ws, a, kModeKeys, flags, stream);
-    if (st != QKD_OK || a.spec_cap == 0 || ws->spec_stat_pending) return st;
+    if (st != QKD_OK || a.spec_cap == 0 || a.ckpt_unsat || ws->spec_stat_pending) return st;
     if (!ws->spec_stat_host) {
         if (hipHostMalloc(reinterpret_cast<void**>(&ws->spec_stat_host), 8, hipHostMallocDefault) != hipSuccess ||
             hipEventCreateWithFlags(&ws->spec_stat_ev, hipEventDisableTiming) != hipSuccess)

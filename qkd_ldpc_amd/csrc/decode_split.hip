@@ -382,7 +382,12 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
 // instantiation compiles with a shorter bit-phase load batch (kBitChunkSpec)
 // to leave the registers to the interval phases. The replay policy (ctl[6])
 // can send a frame straight to the exact iterations.
-template <int MODE, int RULE, int DC, bool CLAMP, bool SPEC>
+// SPEC 2 (checkpointed, keys path, for QBERs where most frames fail the
+// above): the exact iterations come first; once one leaves at most
+// a.ckpt_unsat checks unsatisfied the message store is saved (a.ckpt) and
+// the iterations go on with intervals; a frame they cannot certify within
+// spec_cap iterations resumes exactly from the saved messages.
+template <int MODE, int RULE, int DC, bool CLAMP, int SPEC>
 __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a) {
     using T = typename RuleMsg<RULE>::T;
     constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
@@ -417,8 +422,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     const bool fold1 = TABLES && a.first_table && c.max_dv <= kDvUnroll;
     const bool tab2_on = fold1 && a.tab2_entries;
     uint32_t rnd = 0;    // rounds (iterations of any frame) run by this workgroup
-    if (tid == 0) { ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
+    if (tid == 0) { ctl[2] = 0; ctl[3] = 0; ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
     static_assert(!SPEC || (RULE == kRuleSp64 && CLAMP), "speculation: binary64 rule, clamped messages");
+    constexpr bool CKPT = SPEC == 2;
+    static_assert(!CKPT || MODE == kModeKeys, "checkpointed speculation: keys path");
 #ifndef QKD_EXACT_CHUNK
 #define QKD_EXACT_CHUNK kBitChunk
 #endif
@@ -473,7 +480,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
         // kDecodeBlock; N <= 32 * kDecodeBlock, kMaxBitsLds). Without the fold
         // the first check phase reads b2c = LLR_i (:188) from every slot.
         // (the speculative kernel's replay policy for this frame: ctl[6])
-        const bool spec0 = SPEC && ctl[6] != 0;
+        const bool spec0 = SPEC == 1 && ctl[6] != 0;
         uint32_t bobmask = 0;
         // the first check phase's b2c = LLR_i in every slot (:188), as enclosing
         // intervals when speculating (the LLR path has no folded first iteration)
@@ -520,9 +527,30 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
         bool spec = spec0;
         // a frame the policy keeps off the speculation counts as replayed (so
         // the policy, once on, stays on, and the call's count reports it)
-        if (SPEC && !spec && tid == 0) atomicAdd(a.replay_count, 1u);
+        if (SPEC == 1 && !spec && tid == 0) atomicAdd(a.replay_count, 1u);
         bool done = false;
         uint32_t it = 0;
+        // checkpointed speculation: the iteration the saved messages feed, and
+        // the unsatisfied-check count below which this frame takes its next
+        // checkpoint (halved after each restore; 0 once the policy, ctl[6], is off)
+        uint32_t it_ck = 0;
+        uint32_t ck_lim = (CKPT && ctl[6] != 0) ? a.ckpt_unsat : 0u;
+        // save (and turn into enclosing intervals) or restore every slot
+        auto ckpt_io = [&](bool save) {
+            if constexpr (CKPT) {
+                double* bk = a.ckpt + (size_t)blockIdx.x * a.ckpt_stride;
+                const uint32_t tot = (uint32_t)c.max_dv * n_pad;
+                for (uint32_t x = tid; x < tot; x += kDecodeBlock) {
+                    if (save) {
+                        const T v = ms.ld(x);
+                        bk[x] = v;
+                        ms.st(x, qkds::pack_iv(qkds::iv_of(v)));
+                    } else {
+                        ms.st(x, bk[x]);
+                    }
+                }
+            }
+        };
         for (;;) {
             if (it >= a.max_it) break;
             const bool folded = fold1 && it == 0;
@@ -665,12 +693,18 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // abort, bit 2 some check's parity uncertain (speculative rounds).
             // The next round's word was last read before this round's phases
             // and is next written after the barrier below.
-            if (tid == 0) ctl[4 + ((rnd + 1) & 1u)] = 0;
+            if (tid == 0) {
+                ctl[4 + ((rnd + 1) & 1u)] = 0;
+                if (CKPT) ctl[2 + ((rnd + 1) & 1u)] = 0;
+            }
             // syndrome test (:285): any word differing from the target
             bool mismatch = false, uncertain = false;
+            uint32_t nbad = 0;      // checkpointed speculation: unsatisfied checks
             for (int w = tid; w < m_words; w += kDecodeBlock) {
                 const uint32_t u = xunc[w];
-                mismatch |= ((xsyn[w] ^ tsyn[w]) & ~u) != 0;
+                const uint32_t d = (xsyn[w] ^ tsyn[w]) & ~u;
+                mismatch |= d != 0;
+                if (CKPT) nbad += __builtin_popcount(d);
                 uncertain |= u != 0;
                 xsyn[w] = 0;
                 xunc[w] = 0;
@@ -678,8 +712,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             const uint32_t wv = __builtin_amdgcn_readfirstlane(
                 (uint32_t)(__any(mismatch) ? 1u : 0u) | (uint32_t)(__any(uncertain) ? 4u : 0u));
             if (wv && lane == 0) atomicOr(rw, wv);
+            if (CKPT && nbad) atomicAdd(ctl + 2 + (rnd & 1u), nbad);
             __syncthreads();
             const uint32_t fl = *rw;
+            const uint32_t unsat = CKPT ? ctl[2 + (rnd & 1u)] : 0u;
             rnd++;
             pc.mark(3);
             // A speculative round stands if no sign was lost on the way (bit 1)
@@ -688,10 +724,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // whose hard decision is the output and must then be certain too;
             // or no uncertainty at all (bit 2 clear: the decision is exact).
             if (spec && ((fl & 2u) || ((fl & 4u) && (!(fl & 1u) || it + 1 >= a.max_it)))) {
-                // decode the frame exactly
+                // decode the frame exactly (from its checkpoint)
                 spec = false;
-                it = 0;
-                if (!fold1) {           // the LLR path starts from LLR_i in every slot again
+                it = it_ck;
+                if (CKPT) {
+                    ckpt_io(false);
+                    __syncthreads();
+                    ck_lim >>= 1;
+                } else if (!fold1) {    // the LLR path starts from LLR_i in every slot again
                     init_slots(false);
                     __syncthreads();
                 }
@@ -708,10 +748,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             }
 #endif
             ++it;
-            if (spec && it >= a.spec_cap && it < a.max_it) {
+            if (spec && it >= it_ck + a.spec_cap && it < a.max_it) {
                 spec = false;
-                it = 0;
-                if (!fold1) {
+                it = it_ck;
+                if (CKPT) {
+                    ckpt_io(false);
+                    __syncthreads();
+                    ck_lim >>= 1;
+                } else if (!fold1) {
                     init_slots(false);
                     __syncthreads();
                 }
@@ -719,6 +763,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     atomicAdd(a.replay_count, 1u);
                     atomicAdd(a.spec_replays, 1ull);
                 }
+            } else if (CKPT && !spec && it >= 2 && it + 1 < a.max_it && unsat < ck_lim) {
+                // (exact round: iteration it - 1 left its b2c in the slots, and
+                // iteration it can read intervals of them; iteration 1's slots
+                // are table indices)
+                ckpt_io(true);
+                __syncthreads();
+                spec = true;
+                it_ck = it;
             }
         }
 
@@ -861,7 +913,7 @@ hipError_t launch_key_match(const DecodeArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <int MODE, int RULE, bool CLAMP, bool SPEC = false>
+template <int MODE, int RULE, bool CLAMP, int SPEC = 0>
 static DecodeFn pick_split_dc(int max_dc, int* dc) {
     if (max_dc <= 4) { *dc = 4; return decode_split_kernel<MODE, RULE, 4, CLAMP, SPEC>; }
     if (max_dc <= 6) { *dc = 6; return decode_split_kernel<MODE, RULE, 6, CLAMP, SPEC>; }
@@ -871,9 +923,10 @@ static DecodeFn pick_split_dc(int max_dc, int* dc) {
     return decode_split_kernel<MODE, RULE, 64, CLAMP, SPEC>;
 }
 
-DecodeFn pick_split_spec(int mode, int max_dc, int* dc) {
-    return mode == kModeLlr ? pick_split_dc<kModeLlr, kRuleSp64, true, true>(max_dc, dc)
-                            : pick_split_dc<kModeKeys, kRuleSp64, true, true>(max_dc, dc);
+DecodeFn pick_split_spec(int mode, int max_dc, bool ckpt, int* dc) {
+    if (ckpt) return pick_split_dc<kModeKeys, kRuleSp64, true, 2>(max_dc, dc);
+    return mode == kModeLlr ? pick_split_dc<kModeLlr, kRuleSp64, true, 1>(max_dc, dc)
+                            : pick_split_dc<kModeKeys, kRuleSp64, true, 1>(max_dc, dc);
 }
 
 template <int MODE, int RULE>

@@ -15,6 +15,10 @@ namespace qkd {
 // Speculative interval iterations per frame before the exact fallback
 // (decode_split.hip; QKD_SPEC_CAP overrides).
 constexpr int kSpecCapDefault = 8;
+constexpr int kCkptUnsatDefault = 128;    // checkpointed speculation trigger (unsatisfied checks)
+// across calls: a QBER whose speculative call replayed more than this fraction
+// of its frames switches to the checkpointed speculation (decode_keys)
+constexpr double kSpecCkptSwitch = 1.0 / 16.0;
 // Replay fraction above which speculation stops: within a launch for the
 // frames still to start (decode_split.hip), across calls for that QBER and up.
 constexpr double kSpecReplayMax = 1.0 / 6.0;
@@ -103,6 +107,13 @@ struct DecodeArgs {
     // frames replayed exactly in this launch (zeroed per launch): once they
     // pass a quarter of the frames started, later frames skip the speculation
     uint32_t* replay_count;
+    // checkpointed speculation (SPEC 2, high QBER): once an exact iteration
+    // leaves at most ckpt_unsat checks unsatisfied, the messages are saved to
+    // ckpt (ckpt_stride elements per workgroup) and the iterations continue on
+    // intervals; a frame they cannot certify resumes exactly from the save
+    double* ckpt;
+    uint32_t ckpt_stride;
+    uint32_t ckpt_unsat;
 };
 
 // Phase-clock accumulation (diagnostic; a wave-uniform test when off). Each
@@ -418,8 +429,10 @@ using DecodeFn = void (*)(DecodeArgs);
 // decode_split.hip: the split-store kernel for (mode, rule in {kRuleSp64,
 // kRuleSp32}, clamp, check-degree bucket); *dc receives the bucket.
 DecodeFn pick_split_decode(int mode, int rule, bool clamp, int max_dc, int* dc);
-// The speculative kernel (binary64 rule, clamp on) for a mode.
-DecodeFn pick_split_spec(int mode, int max_dc, int* dc);
+// The speculative kernel (binary64 rule, clamp on) for a mode; ckpt: the
+// checkpointed variant (keys path: exact iterations first, interval ones from
+// a checkpoint once few checks are unsatisfied).
+DecodeFn pick_split_spec(int mode, int max_dc, bool ckpt, int* dc);
 // decode_split.hip, kModeKeys: the kernels around the split decoder.
 // Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.
 hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream);

@@ -92,14 +92,17 @@ struct qkd_workspace {
     hipEvent_t done = nullptr;
     // speculation policy across calls (decode.hip, decode_keys): the replay
     // count of the last speculative call comes back asynchronously; a QBER
-    // point whose frames were replayed too often turns the speculation off for
-    // it and every higher QBER on this workspace
+    // point whose frames were replayed too often (kSpecCkptSwitch) switches it
+    // and every higher QBER on this workspace to the checkpointed speculation
     uint32_t* spec_stat_host = nullptr;     // pinned: replays of the last call
     hipEvent_t spec_stat_ev = nullptr;
     bool spec_stat_pending = false;
     double spec_stat_q = 0.0;
     size_t spec_stat_frames = 0;
-    double spec_off_q = 2.0;
+    double spec_ckpt_q = 2.0;
+    // checkpointed speculation: one saved message store per resident workgroup
+    double* ckpt = nullptr;
+    size_t ckpt_slots = 0;
 };
 
 struct qkd_code {

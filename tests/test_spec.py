@@ -192,9 +192,11 @@ def test_spec_llr_path_matches_oracle(Q, H, oracle_code, monkeypatch, cap, q):
 def test_spec_policy_turns_off_at_high_qber(Q, H, golden_vectors, monkeypatch):
     """At QBER 0.08 most frames cannot be certified: the first call replays
     many (the in-launch policy stops speculating after a sixth), later calls on
-    the workspace skip the speculation for that QBER and up; the results are
-    the golden ones throughout."""
+    the workspace skip the speculation for that QBER and up (QKD_CKPT_UNSAT=0:
+    no checkpointed speculation either); the results are the golden ones
+    throughout."""
     monkeypatch.setenv("QKD_SPEC_CAP", "8")
+    monkeypatch.setenv("QKD_CKPT_UNSAT", "0")
     seeds = seeds_dev(Q.make_seeds(777, 10000))
     grid = golden_vectors["c3_qnom"]
     s = int(np.argmin(np.abs(grid - 0.08)))
@@ -209,3 +211,72 @@ def test_spec_policy_turns_off_at_high_qber(Q, H, golden_vectors, monkeypatch):
         counts.append(Q.spec_replays(ws))
     print("replays per call at QBER 0.08:", counts)
     assert counts[0] > 0 and counts[-1] == 0
+
+
+@pytest.mark.parametrize("trigger", ["16", "128", "1024"])
+def test_ckpt_config3_points(Q, H, golden_vectors, monkeypatch, trigger):
+    """Checkpointed speculation (SPEC 2) forced at every config-3 point: exact
+    iterations until fewer than `trigger` checks are unsatisfied, intervals
+    from a saved message store, restores on failure (a trigger of 1024 makes
+    most attempts fail and exercises the restores); golden results."""
+    monkeypatch.setenv("QKD_SPEC_CAP", "8")
+    monkeypatch.setenv("QKD_SPEC_CKPT", "1")
+    monkeypatch.setenv("QKD_CKPT_UNSAT", trigger)
+    seeds = seeds_dev(Q.make_seeds(777, 10000))
+    ws = Q.Workspace(H)
+    grid = golden_vectors["c3_qnom"]
+    total = 0
+    for s, qn in enumerate(grid):
+        Q.spec_replays(ws, reset=True)
+        r = Q.run_trials(H, seeds, float(qn), s, 50, 100.0, True, workspace=ws)
+        torch.cuda.synchronize()
+        assert (r.iterations.cpu().numpy() == golden_vectors["c3_iters"][s]).all(), (trigger, s)
+        assert (r.syndromes_match.cpu().numpy().astype(bool) == golden_vectors["c3_sp"][s]).all()
+        assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c3_ko"][s]).all()
+        n = Q.spec_replays(ws)
+        total += n
+        print(f"trigger {trigger} q {qn:.2f}: {n} restores")
+    if trigger == "1024":
+        assert total > 0
+
+
+@pytest.mark.parametrize("q,max_it,cap", [(0.07, 50, "8"), (0.09, 50, "64"), (0.11, 20, "64"), (0.08, 12, "3")])
+def test_ckpt_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, cap):
+    """Decoded words after checkpointed speculation (converging frames, frames
+    that fail with the intervals running to max_it, caps that force restores)
+    equal the oracle's bit for bit."""
+    monkeypatch.setenv("QKD_SPEC_CAP", cap)
+    monkeypatch.setenv("QKD_SPEC_CKPT", "1")
+    monkeypatch.setenv("QKD_CKPT_UNSAT", "400")
+    rng = np.random.default_rng(int(q * 1000) + max_it)
+    f = 6
+    alice = rng.integers(0, 2, (f, 10240))
+    bob = alice ^ (rng.random((f, 10240)) < q)
+    r = Q.qkd_ldpc(H, torch.from_numpy(alice.astype(np.uint8)).cuda(),
+                   torch.from_numpy(bob.astype(np.uint8)).cuda(), q, max_it, 100.0, True, want_bits=True)
+    torch.cuda.synchronize()
+    its = r.iterations.cpu().numpy()
+    bits = r.bits.cpu().numpy()
+    for k in range(f):
+        want = oracle_code.qkd_ldpc(alice[k], bob[k], q, max_it, 100.0, True)
+        assert its[k] == want["iters"], (q, k)
+        assert bool(r.syndromes_match[k]) == want["sp_ok"] and bool(r.keys_match[k]) == want["key_ok"]
+        assert (bits[k] == want["out"]).all(), (q, k)
+
+
+def test_ckpt_policy_default(Q, H, golden_vectors, monkeypatch):
+    """Default policy at QBER 0.07: the first call speculates from the first
+    iteration and replays too many frames; the next calls switch to the
+    checkpointed speculation; golden results throughout."""
+    monkeypatch.delenv("QKD_SPEC_CAP", raising=False)
+    monkeypatch.delenv("QKD_CKPT_UNSAT", raising=False)
+    monkeypatch.delenv("QKD_SPEC_CKPT", raising=False)
+    seeds = seeds_dev(Q.make_seeds(777, 10000))
+    grid = golden_vectors["c3_qnom"]
+    s = int(np.argmin(np.abs(grid - 0.07)))
+    ws = Q.Workspace(H)
+    for _ in range(3):
+        r = Q.run_trials(H, seeds, float(grid[s]), s, 50, 100.0, True, workspace=ws)
+        torch.cuda.synchronize()
+        assert (r.iterations.cpu().numpy() == golden_vectors["c3_iters"][s]).all()
+        assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c3_ko"][s]).all()
