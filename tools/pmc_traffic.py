@@ -16,7 +16,7 @@ import sys
 
 
 # the headline kernel: the speculative split-store decoder, keys path, binary64
-KERNEL = os.environ.get("QKD_PMC_KERNEL", "decode_split_kernel<1, 0, 6, true, true>")
+KERNEL = os.environ.get("QKD_PMC_KERNEL", "decode_split_kernel<1, 0, 6, true, 1>")
 
 
 def per_launch(d, counter):
