@@ -40,13 +40,12 @@ namespace qkds {
 constexpr float kPhiRel = 0x1.0p-20f;      // relative error allowance of one phi bound (~8 ulp)
 constexpr float kSumRel = 0x1.0p-23f;      // relative allowance per binary32 add (2^-24 is the rounding)
 constexpr float kRefSumAbs = 1.0e-14f;     // reference roundings in the phi domain (absolute)
-constexpr float kPhiHuge = 80.0f;          // phi(x) <= 2 e^-80 < kPhiHugeHi for x >= kPhiHuge
-constexpr float kPhiHugeHi = 4.0e-35f;
+constexpr float kPhiHuge = 80.0f;          // phi evaluated at most here (e^-80: a normal binary32)
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // [lo, hi]; packed binary32 ops
 
 // phi(x) and an upper bound of |phi'(x)| = 1 / sinh(x) (within a factor 2)
-// for finite x > 0 (x >= kPhiHuge: 0, 0).
+// for 0 < x <= kPhiHuge (the callers clamp).
 struct PhiVal {
     float v;
     float slope;
@@ -94,20 +93,19 @@ __device__ __forceinline__ PhiVal phi_eval(float x) {
     // |phi'(x)| = 1 / sinh(x) = 2u / (w (2 - w)) <= 2u / w (2 - w >= 1): an
     // upper bound within a factor 2, which is all the tangent below needs
     o.slope = (2.0f * u) * rw;
-    if (!(x < kPhiHuge)) {
-        o.v = 0.0f;
-        o.slope = 0.0f;
-    }
     return o;
 }
 
 // Bounds of phi over [a, b], 0 < a <= b (finite or +inf): lo <= phi(x) <= hi.
 // phi is decreasing and convex: phi(a) is the maximum, and the tangent at a
-// lies below phi, so phi(a) - (b - a) / sinh(a) is a lower bound.
+// lies below phi, so phi(a) - (b - a) / sinh(a) is a lower bound. Past
+// kPhiHuge both come from a' = kPhiHuge <= a: phi(a') bounds phi(a) above,
+// and the tangent at a' stays below phi on [a', b].
 __device__ __forceinline__ f2 phi_bounds(float a, float b) {
-    const PhiVal e = phi_eval(a);
-    const float hi = a < kPhiHuge ? __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f : kPhiHugeHi;
-    const float t = __builtin_fmaf(-e.slope * (1.0f + 2.0f * kPhiRel), b - a, e.v * (1.0f - kPhiRel));
+    const float a1 = __builtin_fminf(a, kPhiHuge);
+    const PhiVal e = phi_eval(a1);
+    const float hi = __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f;
+    const float t = __builtin_fmaf(-e.slope * (1.0f + 2.0f * kPhiRel), b - a1, e.v * (1.0f - kPhiRel));
     return f2{t > 0.0f ? t : 0.0f, hi};     // lo: also for b = inf (t = -inf) and NaN
 }
 __device__ __forceinline__ void phi_bounds(float a, float b, float& lo, float& hi) {
@@ -117,16 +115,16 @@ __device__ __forceinline__ void phi_bounds(float a, float b, float& lo, float& h
 }
 
 // Bounds of phi over [S_lo, S_hi], 0 <= S_lo <= S_hi: at S_lo = 0 (the
-// widened sum reached zero) the maximum is +inf and the minimum phi(S_hi) is
-// evaluated directly; otherwise one evaluation at S_lo and its tangent.
+// widened sum reached zero) the maximum is +inf and the minimum is taken at
+// S_hi; otherwise one evaluation at S_lo and its tangent (both clamped to
+// kPhiHuge as in phi_bounds).
 __device__ __forceinline__ f2 phi_bounds_out(float s_lo, float s_hi) {
     const bool zero = !(s_lo > 0.0f);
-    const float at = zero ? s_hi : s_lo;
+    const float at = __builtin_fminf(zero ? s_hi : s_lo, kPhiHuge);
     const PhiVal e = phi_eval(at);
-    const float vmax = at < kPhiHuge ? __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f : kPhiHugeHi;
-    const float vmin = e.v * (1.0f - kPhiRel);
-    const float tan = __builtin_fmaf(-e.slope * (1.0f + 2.0f * kPhiRel), s_hi - s_lo, vmin);
-    return f2{zero ? vmin : (tan > 0.0f ? tan : 0.0f), zero ? __builtin_inff() : vmax};
+    const float vmax = __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f;
+    const float tan = __builtin_fmaf(-e.slope * (1.0f + 2.0f * kPhiRel), s_hi - at, e.v * (1.0f - kPhiRel));
+    return f2{tan > 0.0f ? tan : 0.0f, zero ? __builtin_inff() : vmax};
 }
 __device__ __forceinline__ void phi_bounds_out(float s_lo, float s_hi, float& lo, float& hi) {
     const f2 r = phi_bounds_out(s_lo, s_hi);
