@@ -201,15 +201,19 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
         const int deg = pw_deg(w);
         // extrinsic sum over the other lanes of the segment (a subtraction of
         // the own term would widen the interval by the own term's width)
+        // (weight of entry k: bit k of the segment's mask without this lane)
         f2 sum = f2{0.0f, 0.0f};
+        const uint32_t wmask = ((1u << deg) - 1u) & ~(1u << (uint32_t)(lane - start));
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             const f2 o = qkds::unpack_iv(row[start + k]);
-            sum = __builtin_elementwise_fma(o, f2((k < deg && start + k != lane) ? 1.0f : 0.0f), sum);
+            sum = __builtin_elementwise_fma(o, f2((float)((wmask >> k) & 1u)), sum);
         }
-        // widened by the binary32 roundings (relative to the sum) and the
+        // widened by the binary32 roundings (relative to the sum; small
+        // buckets charge every segment the bucket's count) and the
         // reference's binary64 roundings (absolute, qkd_spec.h)
-        const float mg = __builtin_fmaf(sum.y, (float)(deg + 2) * qkds::kSumRel, qkds::kRefSumAbs);
+        const float nr = DC <= 8 ? (float)(DC + 2) : (float)(deg + 2);
+        const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
         f2 ext = sum + f2{-mg, mg};
         ext.x = ext.x > 0.0f ? ext.x : 0.0f;
         bad |= !(ext.y < 600.0f);                          // the reference's product would underflow
