@@ -83,20 +83,17 @@ struct SplitStore {
         BufIo<T>::st(g, in ? kOob : (x - S) * (uint32_t)sizeof(T), v);
     }
     // slots x .. x + 63 of a wave's 64 consecutive lanes (xw = the wave's
-    // first slot, wave-uniform): one kind of access when the wave's slots are
-    // all in LDS or all global
+    // first slot, wave-uniform, a multiple of 64 as S is: SplitLds): all in
+    // LDS or all global, one kind of access
     __device__ __forceinline__ T ld_row(uint32_t xw, uint32_t x) const {
-        if (xw + 64u <= S) return l[x];
-        if (xw >= S) return BufIo<T>::ld(g, (x - S) * (uint32_t)sizeof(T));
-        return ld(x);
+        if (xw < S) return l[x];
+        return BufIo<T>::ld(g, (x - S) * (uint32_t)sizeof(T));
     }
     __device__ __forceinline__ void st_row(uint32_t xw, uint32_t x, T v) const {
-        if (xw + 64u <= S)
+        if (xw < S)
             l[x] = v;
-        else if (xw >= S)
-            BufIo<T>::st(g, (x - S) * (uint32_t)sizeof(T), v);
         else
-            st(x, v);
+            BufIo<T>::st(g, (x - S) * (uint32_t)sizeof(T), v);
     }
 };
 

@@ -398,7 +398,7 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 //   msg   [S + 64] T             message slots 0 .. S-1 (slots S .. max_dv*n_pad-1
 //                                live in the workgroup's global region), then
 //                                one trash slot per lane
-// S is as many slots as the budget leaves after the rest.
+// S is as many slots as the budget leaves after the rest, in whole 64s.
 struct SplitLds {
     size_t tsyn, xsyn, qsyn, xunc, zw, tval, ctab, tab2, ctl, msg, bytes;
     uint32_t S;
@@ -420,7 +420,9 @@ struct SplitLds {
         const size_t slots = (size_t)max_dv * n_pad;
         // 64 trash slots follow the S message slots (decode_split.hip SplitStore)
         const size_t fit = budget > msg + 64 * (size_t)esz ? (budget - msg) / (size_t)esz - 64 : 0;
-        S = (uint32_t)(slots < fit ? slots : fit);
+        // (a multiple of 64: with n_pad one too, a wave's 64 consecutive bits
+        // of one row are all in LDS or all global, SplitStore::ld_row)
+        S = (uint32_t)(slots < fit ? slots : fit) & ~63u;
         bytes = msg + ((size_t)S + 64) * esz;
     }
 };
