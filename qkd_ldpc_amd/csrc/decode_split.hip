@@ -70,17 +70,18 @@ struct SplitStore {
     T* l;                        // LDS slots [0, S) and the trash slots [S, S + 64)
     __amdgpu_buffer_rsrc_t g;    // global slots S.. of this workgroup
     uint32_t S;
-    static constexpr uint32_t kOob = 0x7ffffff0u;
+    // (for x < S the buffer offset (x - S) * size wraps to at least
+    // 2^32 - S * size, far past the region: out of range without a select)
     __device__ __forceinline__ T ld(uint32_t x) const {
         const bool in = x < S;
         const T vl = l[in ? x : 0u];
-        const T vg = BufIo<T>::ld(g, in ? kOob : (x - S) * (uint32_t)sizeof(T));
+        const T vg = BufIo<T>::ld(g, (x - S) * (uint32_t)sizeof(T));
         return in ? vl : vg;
     }
     __device__ __forceinline__ void st(uint32_t x, T v) const {
         const bool in = x < S;
         l[in ? x : S + (threadIdx.x & 63u)] = v;
-        BufIo<T>::st(g, in ? kOob : (x - S) * (uint32_t)sizeof(T), v);
+        BufIo<T>::st(g, (x - S) * (uint32_t)sizeof(T), v);
     }
     // slots x .. x + 63 of a wave's 64 consecutive lanes (xw = the wave's
     // first slot, wave-uniform, a multiple of 64 as S is: SplitLds): all in
