@@ -235,7 +235,8 @@ QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, con
  * the binary32 variant's tanh(x/2) / 2*atanh(x) (QKD_VARIANT_SP_F32), x
  * rounded to binary32, result widened. which = 4 / 5: certified bounds of
  * phi(x) = -ln tanh(x/2) over [x[2k], x[2k+1]] (the speculative iterations'
- * input / output forms, qkd_spec.h) -> y[2k] = lower, y[2k+1] = upper; n even. */
+ * input / output forms, qkd_spec.h) -> y[2k] = lower, y[2k+1] = upper; n even;
+ * which = 5 takes its interval in log2-domain units (x = S / ln 2). */
 QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
 
 /* ---- host helpers --------------------------------------------------------- */

@@ -1443,12 +1443,19 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
         case 5: {
             // phi bounds over [x[2k], x[2k+1]] -> y[2k] = lo, y[2k+1] = hi
             // (4: qkds::phi_bounds, 5: qkds::phi_bounds_out); one thread per pair
+            // phi_bounds gives psi = phi / ln 2 (returned scaled back to phi in
+            // binary64); phi_bounds_out takes psi-unit sums (x = S / ln 2)
             if (i & 1) break;
             float lo, hi;
-            if (which == 4) qkds::phi_bounds((float)x[i], (float)x[i + 1], lo, hi);
-            else qkds::phi_bounds_out((float)x[i], (float)x[i + 1], lo, hi);
-            y[i] = lo;
-            y[i + 1] = hi;
+            if (which == 4) {
+                qkds::phi_bounds((float)x[i], (float)x[i + 1], lo, hi);
+                y[i] = (double)lo * 0.6931471805599453;
+                y[i + 1] = (double)hi * 0.6931471805599453;
+            } else {
+                qkds::phi_bounds_out((float)x[i], (float)x[i + 1], lo, hi);
+                y[i] = lo;
+                y[i + 1] = hi;
+            }
             break;
         }
         case 6: y[i] = (double)__builtin_amdgcn_exp2f((float)x[i]); break;   // hardware v_exp_f32

@@ -191,7 +191,7 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
         // dummy column) do not count
         const bool ok = (neg || bv.x > 0.0f) && ab.x > 1.0e-30f;
         bad |= !ok && pw_bit(w) != n_bits;
-        const f2 ph = ok ? qkds::phi_bounds(ab.x, ab.y) : f2{0.0f, 0.0f};   // phi(|b2c|)
+        const f2 ph = ok ? qkds::phi_bounds(ab.x, ab.y) : f2{0.0f, 0.0f};   // phi(|b2c|) / ln 2
         row[lane] = qkds::pack_iv(ph);
         const uint64_t sgn = __ballot(neg);
         wave_lds_sync();
@@ -214,7 +214,7 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
         const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
         f2 ext = sum + f2{-mg, mg};
         ext.x = ext.x > 0.0f ? ext.x : 0.0f;
-        bad |= !(ext.y < 600.0f);                          // the reference's product would underflow
+        bad |= !(ext.y < qkds::kPsiSumMax);                // the reference's product would underflow
         f2 m = qkds::phi_bounds_out(ext.x, ext.y);
         // threshold_matrix (:246-249) on the magnitude
         m.x = __builtin_fminf(m.x, thr_dn);

@@ -25,7 +25,7 @@
 // P / t is exactly +-1 (message +-inf, clamped to +-thr): the widened sum then
 // reaches 0 and the upper bound becomes inf (then thr).
 //
-// binary32 evaluation errors: phi_eval's value and slope are within a few ulp
+// binary32 evaluation errors: phi_core's value and slope are within a few ulp
 // (hardware v_exp_f32 / v_log_f32 after an exact argument split); every bound
 // is widened by kPhiRel (2^-20, ~8 ulp; measured use under a third of it)
 // relative plus tiny absolute terms.
@@ -39,28 +39,28 @@ namespace qkds {
 
 constexpr float kPhiRel = 0x1.0p-20f;      // relative error allowance of one phi bound (~8 ulp)
 constexpr float kSumRel = 0x1.0p-23f;      // relative allowance per binary32 add (2^-24 is the rounding)
-constexpr float kRefSumAbs = 1.0e-14f;     // reference roundings in the phi domain (absolute)
+// The check rule sums psi = phi / ln 2 (the log2 domain): the input bounds are
+// produced in it (no ln 2 scaling after the log) and the output evaluation
+// takes 2^-S directly (no argument split).
+constexpr float kLn2 = 0.693147180559945f;
+constexpr float kInvLn2 = 1.44269504088896f;
+constexpr float kRefSumAbs = 1.5e-14f;     // reference roundings (1e-14 in the phi domain), psi units
 constexpr float kPhiHuge = 80.0f;          // phi evaluated at most here (e^-80: a normal binary32)
+constexpr float kPsiHuge = 115.0f;         // the same bound for psi-unit sums (115 ln 2 < 80)
+constexpr float kPsiSumMax = 865.0f;       // 600 / ln 2: the reference's product would underflow
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // [lo, hi]; packed binary32 ops
 
-// phi(x) and an upper bound of |phi'(x)| = 1 / sinh(x) (within a factor 2)
-// for 0 < x <= kPhiHuge (the callers clamp).
+// phi (PSI: phi / ln 2) and an upper bound of |phi'(x)| = 1 / sinh(x)
+// (within a factor 2) at 0 < x <= kPhiHuge from u = e^-x (accurate) and x
+// (for the small-x series and the branch only).
 struct PhiVal {
     float v;
     float slope;
 };
 
-__device__ __forceinline__ PhiVal phi_eval(float x) {
-    // u = e^-x = 2^-(x log2 e), argument split so the reduction is exact to
-    // ~2^-48: p = fl(x * L), r = x * L - p (fma, exact) + x * L_lo
-    const float L = 1.44269502162933349609375f;          // log2(e) rounded to binary32
-    const float L_lo = 1.925963033500011079e-08f;        // log2(e) - L
-    const float p = x * L;
-    const float r = __builtin_fmaf(x, L, -p) + x * L_lo;
-    // 2^-(p + r) = 2^-p (1 - r ln2 + ...), |r| < 2^-17
-    const float e2 = __builtin_amdgcn_exp2f(-p);
-    const float u = __builtin_fmaf(e2, -r * 0.693147180559945f, e2);
+template <bool PSI>
+__device__ __forceinline__ PhiVal phi_core(float x, float u) {
     // w = 1 - u: direct for x >= 0.35 (u <= 0.705: the subtraction costs under
     // a bit), below it the series x (1 - x/2 + x^2/6 - ... + x^6/5040)
     // (truncation < x^7 / 40320 < 1.7e-8 relative)
@@ -77,7 +77,8 @@ __device__ __forceinline__ PhiVal phi_eval(float x) {
     // argument is >= 2.16 (v_log_f32 is accurate to ~2^-22 absolute near 1,
     // so the log is kept away from small results; rcp and the product add
     // 1.5 ulp of the argument)
-    const float vlo = 0.693147180559945f * __builtin_amdgcn_logf(w2 * rw);
+    const float lg = __builtin_amdgcn_logf(w2 * rw);
+    const float vlo = PSI ? lg : kLn2 * lg;
     // x >= 1: phi = 2 atanh(u) = 2u (1 + s/3 + s^2/5 + ... + s^6/13), s = u^2 <= e^-2
     // (truncation < s^7 / 15 (1 + s) < 6.4e-8 relative, under 7 % of kPhiRel)
     const float s = u * u;
@@ -87,25 +88,37 @@ __device__ __forceinline__ PhiVal phi_eval(float x) {
     h = __builtin_fmaf(s, h, 0.2f);
     h = __builtin_fmaf(s, h, 1.0f / 3.0f);
     h = __builtin_fmaf(s, h, 1.0f);
-    const float vhi = (2.0f * u) * h;
+    const float vhi = (u * (PSI ? 2.0f * kInvLn2 : 2.0f)) * h;
     PhiVal o;
     o.v = x < 1.0f ? vlo : vhi;
     // |phi'(x)| = 1 / sinh(x) = 2u / (w (2 - w)) <= 2u / w (2 - w >= 1): an
-    // upper bound within a factor 2, which is all the tangent below needs
+    // upper bound within a factor 2, which is all the tangents below need
     o.slope = (2.0f * u) * rw;
     return o;
 }
 
-// Bounds of phi over [a, b], 0 < a <= b (finite or +inf): lo <= phi(x) <= hi.
-// phi is decreasing and convex: phi(a) is the maximum, and the tangent at a
-// lies below phi, so phi(a) - (b - a) / sinh(a) is a lower bound. Past
-// kPhiHuge both come from a' = kPhiHuge <= a: phi(a') bounds phi(a) above,
-// and the tangent at a' stays below phi on [a', b].
+// u = e^-x = 2^-(x log2 e), argument split so the reduction is exact to
+// ~2^-48: p = fl(x * L), r = x * L - p (fma, exact) + x * L_lo, and
+// 2^-(p + r) = 2^-p (1 - r ln2 + ...), |r| < 2^-17 (r ln2 formed directly)
+__device__ __forceinline__ float exp_neg(float x) {
+    const float L = 1.44269502162933349609375f;          // log2(e) rounded to binary32
+    const float L_lo = 1.925963033500011079e-08f;        // log2(e) - L
+    const float p = x * L;
+    const float rl = __builtin_fmaf(__builtin_fmaf(x, L, -p), kLn2, x * (L_lo * kLn2));
+    const float e2 = __builtin_amdgcn_exp2f(-p);
+    return __builtin_fmaf(e2, -rl, e2);
+}
+
+// Bounds of psi = phi / ln 2 over [a, b], 0 < a <= b (finite or +inf):
+// lo <= psi(x) <= hi. phi is decreasing and convex: phi(a) is the maximum,
+// and the tangent at a lies below phi, so phi(a) - (b - a) / sinh(a) is a
+// lower bound. Past kPhiHuge both come from a' = kPhiHuge <= a: phi(a')
+// bounds phi(a) above, and the tangent at a' stays below phi on [a', b].
 __device__ __forceinline__ f2 phi_bounds(float a, float b) {
     const float a1 = __builtin_fminf(a, kPhiHuge);
-    const PhiVal e = phi_eval(a1);
+    const PhiVal e = phi_core<true>(a1, exp_neg(a1));
     const float hi = __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f;
-    const float t = __builtin_fmaf(-e.slope * (1.0f + 2.0f * kPhiRel), b - a1, e.v * (1.0f - kPhiRel));
+    const float t = __builtin_fmaf(-e.slope * ((1.0f + 2.0f * kPhiRel) * kInvLn2), b - a1, e.v * (1.0f - kPhiRel));
     return f2{t > 0.0f ? t : 0.0f, hi};     // lo: also for b = inf (t = -inf) and NaN
 }
 __device__ __forceinline__ void phi_bounds(float a, float b, float& lo, float& hi) {
@@ -114,16 +127,17 @@ __device__ __forceinline__ void phi_bounds(float a, float b, float& lo, float& h
     hi = r.y;
 }
 
-// Bounds of phi over [S_lo, S_hi], 0 <= S_lo <= S_hi: at S_lo = 0 (the
-// widened sum reached zero) the maximum is +inf and the minimum is taken at
-// S_hi; otherwise one evaluation at S_lo and its tangent (both clamped to
-// kPhiHuge as in phi_bounds).
+// Bounds of phi(S) over psi-unit sums [P_lo, P_hi] (S = P ln 2), 0 <= P_lo
+// <= P_hi: at P_lo = 0 (the widened sum reached zero) the maximum is +inf and
+// the minimum is taken at P_hi; otherwise one evaluation at P_lo and its
+// tangent (both clamped to kPsiHuge as in phi_bounds). u = 2^-P needs no
+// argument split; x = P ln 2 (rounded) only steers the series and branch.
 __device__ __forceinline__ f2 phi_bounds_out(float s_lo, float s_hi) {
     const bool zero = !(s_lo > 0.0f);
-    const float at = __builtin_fminf(zero ? s_hi : s_lo, kPhiHuge);
-    const PhiVal e = phi_eval(at);
+    const float at = __builtin_fminf(zero ? s_hi : s_lo, kPsiHuge);
+    const PhiVal e = phi_core<false>(at * kLn2, __builtin_amdgcn_exp2f(-at));
     const float vmax = __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f;
-    const float tan = __builtin_fmaf(-e.slope * (1.0f + 2.0f * kPhiRel), s_hi - at, e.v * (1.0f - kPhiRel));
+    const float tan = __builtin_fmaf(-e.slope * ((1.0f + 2.0f * kPhiRel) * kLn2), s_hi - at, e.v * (1.0f - kPhiRel));
     return f2{tan > 0.0f ? tan : 0.0f, zero ? __builtin_inff() : vmax};
 }
 __device__ __forceinline__ void phi_bounds_out(float s_lo, float s_hi, float& lo, float& hi) {

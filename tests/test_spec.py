@@ -48,6 +48,18 @@ def replays(Q, ws, reset=True):
     return v.value
 
 
+LN2 = np.log(2.0)
+
+
+def psi_units(x, direction):
+    """Natural-unit sums as the log2-domain binary32 the output form takes
+    (x / ln 2), rounded down (-1), to nearest (0) or up (+1)."""
+    f = (np.asarray(x, np.float64) / LN2).astype(np.float32)
+    if direction:
+        f = np.nextafter(f, np.float32(np.inf if direction > 0 else 0.0))
+    return f.astype(np.float64)
+
+
 def device_phi(Q, which, a, b):
     x = np.empty(2 * a.size, np.float64)
     x[0::2] = a
@@ -74,12 +86,21 @@ def test_phi_bounds_contain_phi(Q, rel):
     b = (a * (1.0 + rel)).astype(np.float32).astype(np.float64)
     b = np.maximum(a, b)
     for which in (4, 5):
-        lo, hi = device_phi(Q, which, a, b)
+        # the output form works on log2-domain sums: an enclosing interval of
+        # [a, b] for containment, the nearest value (its exact phi) for headroom
+        if which == 4:
+            lo, hi = device_phi(Q, which, a, b)
+        else:
+            lo, hi = device_phi(Q, which, psi_units(a, -1), psi_units(b, 1))
         pa, pb = phi64(a), phi64(b)
         assert (lo <= pb).all(), (which, a[lo > pb][:5], lo[lo > pb][:5], pb[lo > pb][:5])
         assert (hi >= pa).all(), (which, a[hi < pa][:5], hi[hi < pa][:5], pa[hi < pa][:5])
         assert (lo >= 0).all()
         if rel == 0.0:
+            if which == 5:
+                an = psi_units(a, 0)
+                lo, hi = device_phi(Q, which, an, an)
+                pa = phi64(an * LN2)
             fin0 = (a < 70) & (pa > 1e-30)
             # headroom: how much of the 2^-20 allowance the evaluation uses
             # (hi = phi~ (1 + 2^-20), phi~ the evaluation)
@@ -96,7 +117,7 @@ def test_phi_bounds_out_at_zero(Q):
     has an infinite upper bound."""
     a = np.array([0.0, 0.0, 1e-14], np.float64)
     b = np.array([1e-14, 3.0, 2e-14], np.float64)
-    lo, hi = device_phi(Q, 5, a, b)
+    lo, hi = device_phi(Q, 5, psi_units(a, -1), psi_units(b, 1))
     assert np.isinf(hi[0]) and np.isinf(hi[1]) and np.isfinite(hi[2])
     assert (lo <= phi64(b)).all()
 
