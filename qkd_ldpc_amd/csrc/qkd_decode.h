@@ -200,7 +200,10 @@ struct DecodeLds {
 // (bits tid + r*kDecodeBlock) per load batch.
 constexpr int kDvUnroll = 3;
 constexpr int kBitChunk = 5;
-constexpr int kBitChunkSpec = 2;     // the exact iterations inside the speculative kernel
+#ifndef QKD_SPEC_EXACT_CHUNK
+#define QKD_SPEC_EXACT_CHUNK 2
+#endif
+constexpr int kBitChunkSpec = QKD_SPEC_EXACT_CHUNK;     // the exact iterations inside the speculative kernel
 // the second-iteration table index and the first-message fold read a bit's
 // messages from the unrolled rows only
 static_assert(kTab2MaxDv <= kDvUnroll, "tables need every row of their bits unrolled");
