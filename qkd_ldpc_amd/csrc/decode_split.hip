@@ -217,8 +217,10 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
         bad |= !(ext.y < qkds::kPsiSumMax);                // the reference's product would underflow
         f2 m = qkds::phi_bounds_out(ext.x, ext.y);
         // threshold_matrix (:246-249) on the magnitude
-        m.x = __builtin_fminf(m.x, thr_dn);
-        m.y = __builtin_fminf(m.y, thr_up);
+        // (m >= 0, not NaN: med3 with 0 is the min, without the per-edge
+        // canonicalisation fminf needs for a kernel argument)
+        m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
+        m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
         const uint32_t j = pw_chk(w);
         const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
         const uint32_t sigma =

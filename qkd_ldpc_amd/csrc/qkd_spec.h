@@ -115,7 +115,7 @@ __device__ __forceinline__ float exp_neg(float x) {
 // lower bound. Past kPhiHuge both come from a' = kPhiHuge <= a: phi(a')
 // bounds phi(a) above, and the tangent at a' stays below phi on [a', b].
 __device__ __forceinline__ f2 phi_bounds(float a, float b) {
-    const float a1 = __builtin_fminf(a, kPhiHuge);
+    const float a1 = __builtin_amdgcn_fmed3f(a, 0.0f, kPhiHuge);     // min(a, kPhiHuge), a > 0
     const PhiVal e = phi_core<true>(a1, exp_neg(a1));
     const float hi = __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f;
     const float t = __builtin_fmaf(-e.slope * ((1.0f + 2.0f * kPhiRel) * kInvLn2), b - a1, e.v * (1.0f - kPhiRel));
