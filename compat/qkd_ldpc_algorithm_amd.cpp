@@ -16,7 +16,8 @@
 //
 // Code objects: the first call with an H_matrix uploads it (validated CSR +
 // device layouts) and caches the handle by the matrix's row-pointer array;
-// the reference never mutates an H_matrix after reading it. Each host thread
+// each later call checks the cached rows against the matrix's (an address can
+// be reused by a different matrix after free_matrix_H). Each host thread
 // gets its own HIP stream and workspaces, so the reference's thread pool may
 // call these functions concurrently.
 #include <hip/hip_runtime_api.h>
@@ -65,10 +66,26 @@ struct CodeKey {
     }
 };
 
+// A cached code keeps the adjacency it was built from. The reference frees
+// matrices and reads new ones (free_matrix_H, array_and_matrix_operations.cpp:88-94;
+// simulation.cpp:108,134), so a different matrix can reappear at a reused row-pointer
+// address with the same n and m: every hit re-compares the rows (O(E) int compares,
+// microseconds against a device call) and a mismatch rebuilds the entry.
+struct CachedCode {
+    qkd_code* code = nullptr;
+    std::vector<int32_t> ptr, idx;
+};
+
 std::mutex g_codes_mu;
-std::map<CodeKey, qkd_code*>& codes() {
-    static std::map<CodeKey, qkd_code*> m;
+std::map<CodeKey, CachedCode>& codes() {
+    static std::map<CodeKey, CachedCode> m;
     return m;
+}
+// Superseded code objects stay alive: per-thread workspaces are keyed by the
+// qkd_code pointer, so a retired object must never be freed and its address reused.
+std::vector<qkd_code*>& retired_codes() {
+    static std::vector<qkd_code*> v;
+    return v;
 }
 
 // Row length the reference loops over: max weights for the regular twins
@@ -77,23 +94,39 @@ size_t check_row_len(const H_matrix& H, size_t j) {
     return H.is_regular || !H.check_nodes_weight ? H.max_check_nodes_weight : (size_t)H.check_nodes_weight[j];
 }
 
+bool same_rows(const H_matrix& H, const CachedCode& c) {
+    for (size_t j = 0; j < H.num_check_nodes; ++j) {
+        const size_t len = check_row_len(H, j);
+        if ((size_t)(c.ptr[j + 1] - c.ptr[j]) != len) return false;
+        if (len && std::memcmp(H.check_nodes[j], c.idx.data() + c.ptr[j], len * sizeof(int32_t)) != 0)
+            return false;
+    }
+    return true;
+}
+
 qkd_code* code_for(const H_matrix& H) {
+    if (!H.check_nodes || H.num_bit_nodes == 0 || H.num_check_nodes == 0)
+        throw std::runtime_error("H_matrix is empty");
     const CodeKey key{H.check_nodes, H.num_bit_nodes, H.num_check_nodes};
     std::lock_guard<std::mutex> lk(g_codes_mu);
     auto it = codes().find(key);
-    if (it != codes().end()) return it->second;
-    if (!H.check_nodes || H.num_bit_nodes == 0 || H.num_check_nodes == 0)
-        throw std::runtime_error("H_matrix is empty");
-    std::vector<int32_t> ptr(H.num_check_nodes + 1, 0), idx;
+    if (it != codes().end()) {
+        if (same_rows(H, it->second)) return it->second.code;
+        retired_codes().push_back(it->second.code);
+        codes().erase(it);
+    }
+    CachedCode cc;
+    cc.ptr.assign(H.num_check_nodes + 1, 0);
     for (size_t j = 0; j < H.num_check_nodes; ++j) {
-        for (size_t k = 0; k < check_row_len(H, j); ++k) idx.push_back(H.check_nodes[j][k]);
-        ptr[j + 1] = (int32_t)idx.size();
+        for (size_t k = 0; k < check_row_len(H, j); ++k) cc.idx.push_back(H.check_nodes[j][k]);
+        cc.ptr[j + 1] = (int32_t)cc.idx.size();
     }
     qkd_status st = QKD_OK;
-    qkd_code* c = qkd_code_create((int32_t)H.num_bit_nodes, (int32_t)H.num_check_nodes, ptr.data(), idx.data(),
-                                  device_index(), &st);
-    if (!c) fail("qkd_code_create");
-    codes().emplace(key, c);
+    cc.code = qkd_code_create((int32_t)H.num_bit_nodes, (int32_t)H.num_check_nodes, cc.ptr.data(), cc.idx.data(),
+                              device_index(), &st);
+    if (!cc.code) fail("qkd_code_create");
+    qkd_code* c = cc.code;
+    codes().emplace(key, std::move(cc));
     return c;
 }
 

@@ -68,17 +68,44 @@ def _ptr(t) -> int | None:
     return int(t.data_ptr())
 
 
-def _stream(stream) -> int | None:
+def _stream(stream, device: int) -> int | None:
+    """The launch stream: the caller's, else torch's current stream of the code's device
+    (not of whatever device happens to be current)."""
     if stream is None:
-        return int(torch.cuda.current_stream().cuda_stream)
+        return int(torch.cuda.current_stream(device).cuda_stream)
     if isinstance(stream, int):
         return stream
     return int(stream.cuda_stream)
 
 
-def _need_cuda(t, dtype, name):
-    if not (t.is_cuda and t.dtype == dtype and t.is_contiguous()):
+def _need_cuda(t, dtype, name, H: "HMatrix | None" = None):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == dtype and t.is_contiguous()):
         raise QkdError(N.ERR_INVALID_ARG, f"{name} must be a contiguous {dtype} CUDA tensor")
+    if H is not None and t.device.index != H.device:
+        raise QkdError(N.ERR_INVALID_ARG,
+                       f"{name} is on {t.device}, the code lives on cuda:{H.device}")
+
+
+def _frames(t, width: int, name: str, frames: int | None = None) -> int:
+    """Frame count of a [F, width] tensor (a 1-D [width] tensor is one frame). The
+    kernels read F * width elements, so a ragged or short buffer is an error, never
+    a silent floor (the reference's arrays are exactly N or M long)."""
+    if t.dim() == 1 and t.numel() == width:
+        f = 1
+    elif t.dim() == 2 and t.shape[1] == width:
+        f = int(t.shape[0])
+    else:
+        raise QkdError(N.ERR_INVALID_ARG,
+                       f"{name} must have shape [F, {width}], got {list(t.shape)}")
+    if frames is not None and f != frames:
+        raise QkdError(N.ERR_INVALID_ARG, f"{name} holds {f} frames, expected {frames}")
+    return f
+
+
+def _need_vec(t, dtype, count: int, name: str, H: "HMatrix"):
+    _need_cuda(t, dtype, name, H)
+    if t.numel() != count:
+        raise QkdError(N.ERR_INVALID_ARG, f"{name} must hold {count} elements, got {t.numel()}")
 
 
 class HMatrix:
@@ -201,10 +228,10 @@ def spec_replays(ws: Workspace, reset: bool = False) -> int:
 
 def calculate_syndrome(H: HMatrix, bits, stream=None):
     """calculate_syndrome_irregular/_regular: bits [F, N] uint8 -> [F, M] uint8."""
-    _need_cuda(bits, torch.uint8, "bits")
-    f = bits.numel() // H.num_bit_nodes
+    _need_cuda(bits, torch.uint8, "bits", H)
+    f = _frames(bits, H.num_bit_nodes, "bits")
     out = torch.empty((f, H.num_check_nodes), dtype=torch.uint8, device=bits.device)
-    N.check(N.lib().qkd_syndrome_batch(H.handle, _ptr(bits), f, _ptr(out), _stream(stream)))
+    N.check(N.lib().qkd_syndrome_batch(H.handle, _ptr(bits), f, _ptr(out), _stream(stream, H.device)))
     return out
 
 
@@ -231,9 +258,10 @@ def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
                          variant: str = "sp_f64", minsum_scale: float | None = None) -> SPResult:
     """sum_product_decoding_irregular/_regular (qkd_ldpc_algorithm.cpp:3-345), batched.
     llr [F, N] float64, syndrome [F, M] uint8 (0/1)."""
-    _need_cuda(llr, torch.float64, "llr")
-    _need_cuda(syndrome, torch.uint8, "syndrome")
-    f = llr.numel() // H.num_bit_nodes
+    _need_cuda(llr, torch.float64, "llr", H)
+    _need_cuda(syndrome, torch.uint8, "syndrome", H)
+    f = _frames(llr, H.num_bit_nodes, "llr")
+    _frames(syndrome, H.num_check_nodes, "syndrome", f)
     dev = llr.device
     bits = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev) if want_bits else None
     iters = torch.empty(f, dtype=torch.int32, device=dev)
@@ -241,7 +269,7 @@ def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
     flags = decoder_flags(threshold_enabled, variant, minsum_scale)
     N.check(N.lib().qkd_decode_batch(H.handle, _ws(workspace), _ptr(llr), _ptr(syndrome), f,
                                      max_iterations, msg_threshold, flags, _ptr(bits), _ptr(iters),
-                                     _ptr(ok), _stream(stream)))
+                                     _ptr(ok), _stream(stream, H.device)))
     return SPResult(iters, ok, bits)
 
 
@@ -256,9 +284,10 @@ def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
              variant: str = "sp_f64", minsum_scale: float | None = None) -> LDPCResult:
     """QKD_LDPC_irregular/_regular (qkd_ldpc_algorithm.cpp:347-447), batched.
     alice, bob [F, N] uint8 (0/1); one QBER for the batch."""
-    _need_cuda(alice, torch.uint8, "alice")
-    _need_cuda(bob, torch.uint8, "bob")
-    f = alice.numel() // H.num_bit_nodes
+    _need_cuda(alice, torch.uint8, "alice", H)
+    _need_cuda(bob, torch.uint8, "bob", H)
+    f = _frames(alice, H.num_bit_nodes, "alice")
+    _frames(bob, H.num_bit_nodes, "bob", f)
     dev = alice.device
     bits = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev) if want_bits else None
     iters = torch.empty(f, dtype=torch.int32, device=dev)
@@ -267,7 +296,7 @@ def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
     flags = decoder_flags(threshold_enabled, variant, minsum_scale)
     N.check(N.lib().qkd_qkd_ldpc_batch(H.handle, _ws(workspace), _ptr(alice), _ptr(bob), f, qber,
                                        max_iterations, msg_threshold, flags, _ptr(bits),
-                                       _ptr(iters), _ptr(ok), _ptr(km), _stream(stream)))
+                                       _ptr(iters), _ptr(ok), _ptr(km), _stream(stream, H.device)))
     return LDPCResult(iters, ok, km, bits)
 
 
@@ -279,14 +308,16 @@ def keygen(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0, workspace=
            stream=None):
     """generate_random_bit_array + introduce_errors for frames seeded seeds[k] + seed_offset.
     Returns (alice [F,N] u8, bob [F,N] u8, exact_qber [F] f64) on the device."""
-    _need_cuda(seeds, torch.int64, "seeds")
+    _need_cuda(seeds, torch.int64, "seeds", H)
+    if seeds.dim() != 1:
+        raise QkdError(N.ERR_INVALID_ARG, f"seeds must be 1-D, got {list(seeds.shape)}")
     f = seeds.numel()
     dev = seeds.device
     a = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
     q = torch.empty(f, dtype=torch.float64, device=dev)
     N.check(N.lib().qkd_keygen_batch(H.handle, _ws(workspace), _ptr(seeds), seed_offset, f,
-                                     q_nominal, _ptr(a), _ptr(b), _ptr(q), _stream(stream)))
+                                     q_nominal, _ptr(a), _ptr(b), _ptr(q), _stream(stream, H.device)))
     return a, b, q
 
 
@@ -307,9 +338,17 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
     """run_trial (simulation.cpp:161-189) for every frame, fused on the device, plus the
     per-QBER-point counters of simulation.cpp:252-312. seeds: int64 CUDA tensor holding
     the uint64 seed bits."""
-    _need_cuda(seeds, torch.int64, "seeds")
+    _need_cuda(seeds, torch.int64, "seeds", H)
+    if seeds.dim() != 1:
+        raise QkdError(N.ERR_INVALID_ARG, f"seeds must be 1-D, got {list(seeds.shape)}")
     f = seeds.numel()
     dev = seeds.device
+    if out is not None:
+        _need_vec(out.iterations, torch.int32, f, "out.iterations", H)
+        _need_vec(out.syndromes_match, torch.uint8, f, "out.syndromes_match", H)
+        _need_vec(out.keys_match, torch.uint8, f, "out.keys_match", H)
+        _need_vec(out.exact_qber, torch.float64, f, "out.exact_qber", H)
+        _need_vec(out.counters, torch.uint8, N.COUNTERS_BYTES, "out.counters", H)
     if out is None:
         out = TrialResults(torch.empty(f, dtype=torch.int32, device=dev),
                            torch.empty(f, dtype=torch.uint8, device=dev),
@@ -321,7 +360,7 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                                      q_nominal, max_iterations, msg_threshold, flags,
                                      _ptr(out.iterations), _ptr(out.syndromes_match),
                                      _ptr(out.keys_match), _ptr(out.exact_qber),
-                                     _ptr(out.counters), _stream(stream)))
+                                     _ptr(out.counters), _stream(stream, H.device)))
     return out
 
 

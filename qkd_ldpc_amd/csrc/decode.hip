@@ -39,14 +39,6 @@
 #include "qkd_decode.h"
 #include "qkd_spec.h"
 
-// Diagnostic builds only (tools/exp_run.sh; never the shipped library): the
-// QKD_EXP_NO_STOP / QKD_EXP_NO_MATH / QKD_EXP_MSG_LOCAL / QKD_EXP_MSG_SMALL
-// macros run a fixed iteration count / drop the tanh-atanh arithmetic / make
-// the check phase's message accesses coalesced / keep them scattered but
-// within 4 KB per row (cache-resident), to split the kernel's time between
-// arithmetic, access pattern and footprint. Results of such
-// builds are wrong by design.
-
 namespace qkd {
 
 // The check phase of one iteration for one wave: tasks wave, wave + NW, ...
@@ -80,13 +72,7 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
     int t = wave;
     if (t >= n_tasks) return;
     const uint2* pl = plan + lane;
-#ifdef QKD_EXP_MSG_LOCAL
-    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p) * n_pad + lane + 64 * (wave & 7); };
-#elif defined(QKD_EXP_MSG_SMALL)
-    auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p) * n_pad + (pw_bit(p) & 511); };
-#else
     auto msg = [&](uint2 p) -> T* { return c2b + pw_row(p) * n_pad + pw_bit(p); };
-#endif
     // the incoming value: a bit total, or (kSrcTable) the tabulated tanh
     auto src = [&](uint2 p) -> T {
         if constexpr (SRC == kSrcTable) return tab2[t2idx[pw_bit(p)] + pw_row(p)];
@@ -570,12 +556,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             }
             const bool any_mismatch = block_any(mismatch, ctl + 2, any_k);
             pc.mark(3);
-#ifndef QKD_EXP_NO_STOP
             if (!any_mismatch) {
                 done = true;
                 break;
             }
-#endif
         }
 
         // ---- outputs: SP_result + last hard decision (+ keys_match)

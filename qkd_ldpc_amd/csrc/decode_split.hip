@@ -124,11 +124,7 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
         if constexpr (SRC == kSrcTable && RULE == kRuleSp64)
             a = tab2[qkdm::lo32(x)];
         else
-#ifdef QKD_EXP_NO_MATH
-            a = x * (T)0.5;
-#else
             a = RuleMath<RULE>::tanh_half(x);                      // (:224)
-#endif
         row[lane] = a;
         wave_lds_sync();
         return edge_out<CLAMP, DC, RULE>(a, w, sbit(w), lane, thr, row, 0.0f);
@@ -434,11 +430,6 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
 #define QKD_EXACT_CHUNK kBitChunk
 #endif
     constexpr int BC = SPEC ? kBitChunkSpec : QKD_EXACT_CHUNK;      // exact bit phase load batch
-#ifdef QKD_EXP_NO_REPLAY
-    constexpr bool EXACT_IN = !SPEC;     // diagnostic: the speculative kernel without its exact path
-#else
-    constexpr bool EXACT_IN = true;
-#endif
     if (TABLES && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
     if (tab2_on) {
         __syncthreads();
@@ -567,7 +558,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                         __syncthreads();
                     }
                 }
-            } else if (EXACT_IN && !folded) {
+            } else if (!folded) {
                 if (TABLES && it == 1 && tab2_on)
                     split_check_phase<kSrcTable, CLAMP, DC, RULE>(c.plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);
@@ -591,7 +582,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                         spec_bit_phase<false, MODE>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, f, tid,
                                                     wave, lane);
                 }
-            } else if (EXACT_IN)
+            } else
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += BC) {
                 T v[BC][kDvUnroll];
                 int32_t jc[BC][kDvUnroll];
@@ -646,11 +637,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     const bool z = ok && acc <= 0;
                     const uint64_t zb = __ballot(z);
                     if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
-#ifdef QKD_EXP_NO_SYN
-                    if (false) {
-#else
                     if (z) {
-#endif
 #pragma unroll
                         for (int k = 0; k < kDvUnroll; ++k)
                             if (k < deg) atomicXor(&xsyn[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
@@ -745,12 +732,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                 }
                 continue;
             }
-#ifndef QKD_EXP_NO_STOP
             if (!(fl & 1u)) {
                 done = true;
                 break;
             }
-#endif
             ++it;
             if (spec && it >= it_ck + a.spec_cap && it < a.max_it) {
                 spec = false;

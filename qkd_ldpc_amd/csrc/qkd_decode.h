@@ -288,9 +288,6 @@ __device__ __forceinline__ T edge_in(T x, T old, T thr) {
         x = x - old;
         if (CLAMP) x = clamp_msg(x, thr);
     }
-#ifdef QKD_EXP_NO_MATH
-    return x * (T)0.5;
-#endif
     if constexpr (RULE == kRuleMinSum) return x;
     else return SRC == kSrcTable ? x : RuleMath<RULE>::tanh_half(x);
 }
@@ -326,11 +323,7 @@ __device__ __forceinline__ T edge_out(T tv, uint2 w, uint32_t sbit, int lane, T 
         P = P * o[0];                         // every check has degree >= 1
 #pragma unroll
         for (int k = 1; k < DC; ++k) P = k < deg ? P * o[k] : P;
-#ifdef QKD_EXP_NO_MATH
-        v = P + tv;
-#else
         v = RuleMath<RULE>::two_atanh(P / tv);
-#endif
     } else {
         // binary32 variant: the extrinsic product over the other edges in
         // ascending order, no division. (P / t is 0/0 = NaN when b2c is

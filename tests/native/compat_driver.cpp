@@ -4,6 +4,9 @@
 // pytest side (tests/test_compat.py) compares them with the oracle.
 //
 //   code <n> <m>                 then m lines "<deg> <bit>..." (0-based, ascending)
+//   recode                       same as code with the current n, m, but the new rows go
+//                                behind the SAME check_nodes pointer array (free_matrix_H
+//                                then a read that reuses the address, simulation.cpp:108,134)
 //   cfg <max_it> <thr> <thr_on> <trials> <seed>
 //   decode                       then a line of n LLRs and a line of m syndrome bits
 //   qkd <q>                      then a line of n alice bits and a line of n bob bits
@@ -76,6 +79,25 @@ int main() {
                 }
                 H = make_matrix(n, m, rows);
                 std::printf("ok code %d\n", (int)H.is_regular);
+            } else if (cmd == "recode") {
+                std::vector<std::vector<int>> rows(H.num_check_nodes);
+                for (size_t j = 0; j < H.num_check_nodes; ++j) {
+                    size_t d;
+                    std::cin >> d;
+                    rows[j] = read_line<int>(d);
+                }
+                int** keep = H.check_nodes;
+                for (size_t j = 0; j < H.num_check_nodes; ++j) delete[] keep[j];
+                for (size_t i = 0; i < H.num_bit_nodes; ++i) delete[] H.bit_nodes[i];
+                delete[] H.bit_nodes;
+                delete[] H.bit_nodes_weight;
+                delete[] H.check_nodes_weight;
+                H_matrix fresh = make_matrix(H.num_bit_nodes, H.num_check_nodes, rows);
+                for (size_t j = 0; j < H.num_check_nodes; ++j) keep[j] = fresh.check_nodes[j];
+                delete[] fresh.check_nodes;
+                fresh.check_nodes = keep;
+                H = fresh;
+                std::printf("ok recode %d\n", (int)H.is_regular);
             } else if (cmd == "cfg") {
                 int on;
                 std::cin >> CFG.SUM_PRODUCT_MAX_ITERATIONS >> CFG.SUM_PRODUCT_MSG_LLR_THRESHOLD >> on >>

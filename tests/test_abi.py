@@ -198,3 +198,51 @@ def test_product_never_imports_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h", ".hpp")):
                 text = open(os.path.join(dirpath, f), errors="replace").read()
                 assert "oracle" not in text.lower() or f == "__init__.py" and "oracle" not in text, f
+
+
+# ---- Python wrapper argument checks (the kernels read F x N / F x M elements) -------
+
+def test_frames_rejects_ragged_and_short_buffers():
+    import torch
+    import qkd_ldpc_amd as Q
+    assert Q._frames(torch.zeros(3, 10), 10, "llr") == 3
+    assert Q._frames(torch.zeros(10), 10, "llr") == 1
+    for bad in (torch.zeros(25), torch.zeros(3, 9), torch.zeros(2, 3, 10)):
+        with pytest.raises(Q.QkdError):
+            Q._frames(bad, 10, "llr")
+    with pytest.raises(Q.QkdError):
+        Q._frames(torch.zeros(2, 5), 5, "syndrome", frames=3)
+
+
+def test_wrappers_reject_host_tensors():
+    import torch
+    import qkd_ldpc_amd as Q
+    with pytest.raises(Q.QkdError):
+        Q._need_cuda(torch.zeros(4, dtype=torch.float64), torch.float64, "llr")
+    with pytest.raises(Q.QkdError):
+        Q._need_cuda(np.zeros(4), torch.float64, "llr")
+
+
+@pytest.mark.gpu
+def test_wrappers_reject_mismatched_shapes(golden_code):
+    import torch
+    import qkd_ldpc_amd as Q
+    g = golden_code
+    H = Q.HMatrix.from_check_lists(10240, g["chk_off"], g["chk_idx"])
+    llr = torch.zeros(4, 10240, dtype=torch.float64, device="cuda")
+    syn = torch.zeros(4, 5231, dtype=torch.uint8, device="cuda")
+    bits = torch.zeros(4, 10240, dtype=torch.uint8, device="cuda")
+    cases = [
+        lambda: Q.sum_product_decoding(H, llr, syn[:3]),                     # short syndrome
+        lambda: Q.sum_product_decoding(H, llr.view(-1)[:-5], syn),           # not a multiple of N
+        lambda: Q.sum_product_decoding(H, llr, syn.view(-1)[:4 * 5230]),     # flat, wrong width
+        lambda: Q.qkd_ldpc(H, bits, bits[:2], 0.02),                          # bob shorter than alice
+        lambda: Q.calculate_syndrome(H, bits[:, :100]),
+        lambda: Q.keygen(H, torch.zeros(2, 2, dtype=torch.int64, device="cuda"), 0.02),
+        lambda: Q.run_trials(H, torch.zeros(4, dtype=torch.int64, device="cuda"), 0.02,
+                             out=Q.run_trials(H, torch.zeros(2, dtype=torch.int64, device="cuda"), 0.02)),
+    ]
+    for k, call in enumerate(cases):
+        with pytest.raises(Q.QkdError):
+            call()
+    torch.cuda.synchronize()

@@ -154,6 +154,44 @@ def test_compat_n10240_decode_trial_batch(driver, golden_code, oracle_code, orac
 
 
 @pytest.mark.gpu
+def test_compat_code_cache_survives_address_reuse(driver, oracle_mod):
+    """A matrix freed and a different one read at the same address with the same n, m
+    (free_matrix_H, array_and_matrix_operations.cpp:88-94; simulation.cpp:108,134) must
+    decode on its own adjacency, not on the shim's cached code object."""
+    rng = np.random.default_rng(5)
+    n, m = 10, 5
+    d1 = np.array([[1, 1, 0, 1, 0, 0, 1, 0, 0, 1], [0, 1, 1, 0, 1, 0, 0, 1, 0, 0],
+                   [1, 0, 1, 0, 0, 1, 0, 0, 1, 0], [0, 0, 0, 1, 1, 0, 1, 1, 0, 0],
+                   [0, 1, 0, 0, 0, 1, 0, 1, 1, 1]], np.uint8)
+    d2 = d1[:, rng.permutation(n)]          # same n, m and weights, different adjacency
+    assert (d2 != d1).any()
+    alice = np.array([1, 0, 1, 1, 0, 0, 1, 1, 0, 1])
+    bob = alice.copy()
+    bob[3] ^= 1
+    q = 0.1
+    lp = np.log((1 - q) / q)
+    llr = np.where(bob == 1, -lp, lp)
+    lines = ["cfg 20 100.0 1 1 777"]
+    want = []
+    for k, dense in enumerate((d1, d2, d1)):
+        off, idx = _dense_lists(dense)
+        rows = _code_cmd(n, m, off, idx)
+        lines += rows if k == 0 else ["recode"] + rows[1:]
+        oc = oracle_mod.Code.from_dense(dense)
+        syn = oc.syndrome(alice)
+        lines += ["decode", _fmt(llr), _fmt(syn), "syndrome", _fmt(alice)]
+        want.append((oc.decode(llr, syn, 20, 100.0, True), syn))
+    out = _run(driver, lines)
+    dec = [ln.split() for ln in out if ln.startswith("decode")]
+    syns = [ln.split()[1:] for ln in out if ln.startswith("syndrome")]
+    assert len(dec) == 3 and len(syns) == 3
+    for v, s, (w, syn) in zip(dec, syns, want):
+        assert int(v[1]) == w["iters"] and bool(int(v[2])) == w["sp_ok"]
+        assert [int(x) for x in v[3:]] == w["out"].tolist()
+        assert [int(x) for x in s] == syn.tolist()
+
+
+@pytest.mark.gpu
 def test_compat_too_small_qber_throws_reference_message(driver):
     lines = _code_cmd(6, 4, [0, 3, 6, 9, 12], [0, 1, 3, 1, 2, 4, 0, 4, 5, 2, 3, 5])
     p = subprocess.run([driver], input="\n".join(lines + ["cfg 10 100.0 1 1 1", "trial 0.01 5"]) + "\n",
