@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=777)
     ap.add_argument("--cpu-frames", type=int, default=8192,
                     help="frames in the CPU-baseline sample (0 disables)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="CPU-baseline threads (capped at the CPUs this process may use)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (keygen + decode) line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", default="sp_f64", choices=["sp_f64", "sp_f32", "minsum"],
                     help="decoder rule of the headline line (sp_f64 = the reference's)")
@@ -67,15 +69,40 @@ def load_code(device):
                                       device=device), g
 
 
-def pmc_traffic():
-    """HBM bytes per decode launch from the newest profiles/*pmc*.json written by
-    tools/pmc_traffic.py (separate rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_decode*.json")))
+# The oracle (oracle/oracle.c) against the reference on the same 8-core Xeon of the
+# build container, config 2 (4096 frames): the reference's 2.66-2.76 s were measured
+# by the survey; the oracle's time is tools/cpu_calibrate.py's.
+REF_C2_8T_S = (2.66, 2.76)
+ORACLE_C2_8T_S = None      # filled in from profiles/cpu_calibration.json when present
+
+
+def pmc_record(variant):
+    """Per-launch PMC record of the variant's decode kernel (newest
+    profiles/r*_pmc_<variant>.json, written by tools/pmc_traffic.py from separate
+    rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{variant}.json")))
     if not files:
-        return None, None, None
+        return None, None
     with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT), d.get("valu_busy")
+        return json.load(f), os.path.relpath(files[-1], ROOT)
+
+
+def roofline_block(variant, alg_bytes, kernel_s, kernel_name):
+    """roofline: algorithmic bytes / the launch's HIP-event time
+    against the 8 TB/s HBM peak (nominal: the formulation here moves fewer bytes),
+    plus what the PMC record measured for the same kernel."""
+    achieved = alg_bytes / kernel_s / 1e9
+    rec, src = pmc_record(variant)
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
+           "nominal": True, "kernel": kernel_name, "kernel_ms": kernel_s * 1e3,
+           "algorithmic_bytes_per_launch": alg_bytes, "traffic_source": src}
+    if rec:
+        out["dram_gbs_measured"] = rec["hbm_bytes_per_launch"] / kernel_s / 1e9
+        if "valu" in rec:
+            out["valu"] = rec["valu"]
+        out["pmc_kernel"] = rec.get("kernel")
+    return out
 
 
 def measure_variants(args, step, stream, counters, iters, Q, F, q, steps=5):
@@ -98,10 +125,44 @@ def measure_variants(args, step, stream, counters, iters, Q, F, q, steps=5):
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         st = Q.counters_to_stats(Q.read_counters(counters), F, args.max_iters, q)
-        out[v] = {"value": F * N_BITS * steps / el, "unit": "bit/s",
-                  "kernel_ms": float(np.mean([a.elapsed_time(b) for a, b in evs])),
-                  "fer": st["fer"], "mean_iterations": st["iterations_successful_sp_mean"]}
+        kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        b_iter = B_ITER if v == "sp_f64" else B_ITER32
+        alg = int(iters.cpu().numpy().astype(np.int64).sum()) * b_iter + F * B_FRAME
+        out[v] = {"value": F * N_BITS * steps / el, "unit": "bit/s", "kernel_ms": kms,
+                  "fer": st["fer"], "mean_iterations": st["iterations_successful_sp_mean"],
+                  "roofline": roofline_block(v, alg, kms / 1e3, f"qkd_qkd_ldpc_batch, variant {v}")}
     return out
+
+
+def measure_end_to_end(args, H, ws, seeds, F, Q, steps):
+    """End to end per SURVEY.md §8(d) / run_trial (simulation.cpp:161-189): device
+    keygen + LLR + syndrome + decode + key compare + counters, one qkd_trials_batch
+    per step from the seeds alone."""
+    import torch
+    res = Q.run_trials(H, seeds, args.qber, 0, args.max_iters, args.threshold, True, workspace=ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        Q.run_trials(H, seeds, args.qber, 0, args.max_iters, args.threshold, True, workspace=ws, out=res)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st = Q.counters_to_stats(Q.read_counters(res.counters), F, args.max_iters,
+                             float(res.exact_qber[0].item()))
+    return {"value": F * N_BITS * steps / el, "unit": "bit/s", "ms_per_step": el * 1e3 / steps,
+            "steps": steps, "fer": st["fer"], "sum_iterations": st["sum_iters_sp"],
+            "what": "qkd_trials_batch: keygen_fast_kernel + frame_syn + decoder + key_match + counters"}
+
+
+def cpu_calibration():
+    p = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    ref = sum(REF_C2_8T_S) / 2
+    return {"oracle_c2_8threads_s": d["oracle_c2_seconds"], "reference_c2_8threads_s": list(REF_C2_8T_S),
+            "oracle_over_reference_time": d["oracle_c2_seconds"] / ref,
+            "where": d.get("host", "build container, 8-core Xeon"), "source": "profiles/cpu_calibration.json"}
 
 
 def cpu_baseline(args, g):
@@ -112,18 +173,29 @@ def cpu_baseline(args, g):
     code = O.Code.from_lists(g)
     frames = args.cpu_frames
     seeds = O.seeds(args.seed, frames)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = max(1, min(args.cpu_threads, avail))
     t0 = time.perf_counter()
     r = code.trials(args.qber, seeds, 0, args.max_iters, args.threshold, True, threads=threads)
     dt = time.perf_counter() - t0
+    cal = cpu_calibration()
     return {
         "value": frames * N_BITS / dt,
         "unit": "bit/s",
+        "reference_equivalent_value": frames * N_BITS / dt * cal["oracle_over_reference_time"] if cal else None,
         "cores": threads,
         "kind": "port",
         "sample": f"{frames} frames of the same config (seeds 777[0:{frames}]), "
                   f"{threads} threads, {dt:.2f} s wall, mean it "
                   f"{float(np.mean(r['iters'])):.4f}",
+        "host_cpus_visible": os.cpu_count(),
+        "host_cpus_affinity": avail,
+        "cores_note": "one thread per core of this GPU's host CPU share (16 per GPU on the "
+                      "MI355X pool; os.cpu_count() shows the whole machine)",
+        "calibration": cal,
     }
 
 
@@ -205,8 +277,6 @@ def main():
     b_iter = B_ITER if args.variant == "sp_f64" else B_ITER32
     alg_bytes = sum_it_local * b_iter + F * B_FRAME
     avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
-    achieved = alg_bytes / avg_kernel_s / 1e9
-    traffic, traffic_src, valu_busy = pmc_traffic()
     replays = Q.spec_replays(ws, reset=True)
 
     stats = Q.counters_to_stats(c, frames_total, args.max_iters, q)
@@ -236,20 +306,10 @@ def main():
             "fer": stats["fer"],
             "mean_iterations": stats["iterations_successful_sp_mean"],
             "sum_iterations": stats["sum_iters_sp"],
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel": "qkd_qkd_ldpc_batch = pack + frame_syn_kernel + decode_split_kernel (speculative) "
-                          "+ key_match_kernel, HIP events on its stream",
-                "kernel_ms": avg_kernel_s * 1e3,
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "traffic_source": traffic_src,
-                "valu_busy_pmc": valu_busy,
-            },
+            "roofline": roofline_block(
+                args.variant, alg_bytes, avg_kernel_s,
+                "qkd_qkd_ldpc_batch = frame_syn_kernel + decode_split_kernel + key_match_kernel "
+                "(+ pack of Alice/Bob), HIP events on its stream"),
             "speculation": {
                 "replayed_frames": replays,
                 "frames": F * (args.steps + args.warmup),
@@ -263,6 +323,8 @@ def main():
             names = ["prologue", "check", "bit", "syndrome", "fetch_out", "check_first", "check_second"]
             tot = float(cyc.sum()) or 1.0
             out["phase_share"] = {n: float(v) / tot for n, v in zip(names, cyc)}
+        if world == 1 and not args.no_e2e:
+            out["end_to_end"] = measure_end_to_end(args, H, ws, seeds, F, Q, args.steps)
         if world == 1 and not args.no_variants:
             out["variants"] = measure_variants(args, step, stream, counters, iters, Q, F, q)
         if world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:

@@ -238,6 +238,18 @@ QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, con
  * input / output forms, qkd_spec.h) -> y[2k] = lower, y[2k+1] = upper; n even;
  * which = 5 takes its interval in log2-domain units (x = S / ln 2). */
 QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
+/* Exhaustive check of the speculative iterations' phi bounds (qkd_spec.h) at
+ * EVERY binary32 a with bit pattern in [first_bits, last_bits] (positive
+ * finite): which = 4 the input form phi_bounds (a in nep units, psi result),
+ * which = 5 the output form phi_bounds_out (a in log2-domain units, S = a ln 2),
+ * both at the degenerate interval [a, a], against a binary64 phi on the
+ * device. result[8] (host): [0] points, [1] upper bound below phi(a),
+ * [2] lower bound above phi(a), [3] slope bound (with half its 2^-20 margin)
+ * below |phi'(a)|, [4] max |eval/phi - 1| / 2^-20 (binary32 bits), [5] max
+ * |phi'| / slope bound (binary32 bits), [6] / [7] bit patterns where [4] / [5]
+ * peak (either of the tied points). Synchronous. Test infrastructure: no
+ * reference counterpart (the reference has no speculative iterations). */
+QKD_API qkd_status qkd_debug_phi_sweep(int which, uint32_t first_bits, uint32_t last_bits, uint64_t *result);
 
 /* ---- host helpers --------------------------------------------------------- */
 /* seeds[k] = k-th raw xoshiro256++(simulation_seed) output (simulation.cpp:222-228). */

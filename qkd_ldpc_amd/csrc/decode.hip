@@ -1459,6 +1459,96 @@ qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void*
     return QKD_OK;
 }
 
+// Exhaustive phi-bound sweep (qkd_debug_phi_sweep): one binary32 point per
+// (thread, step), binary64 phi and |phi'| from OCML's exp / expm1 / log1p
+// (about 1 ulp of binary64, 2^-32 of the 2^-20 allowance).
+__device__ __forceinline__ void sweep_max(float v, uint32_t bits, uint32_t* mx, uint32_t* at) {
+    const uint32_t b = __builtin_bit_cast(uint32_t, v);
+    if (b > atomicMax(mx, b)) atomicExch(at, bits);
+}
+
+__global__ void phi_sweep_kernel(int which, uint32_t first, uint32_t last, unsigned long long* cnt,
+                                 uint32_t* mx) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long pts = 0, bad_hi = 0, bad_lo = 0, bad_sl = 0;
+    float e_max = 0.0f, s_max = 0.0f;
+    uint32_t e_at = 0, s_at = 0;
+    constexpr double R = 0x1.0p-20;
+    for (uint64_t k = (uint64_t)first + blockIdx.x * blockDim.x + threadIdx.x; k <= last; k += stride) {
+        const uint32_t bits = (uint32_t)k;
+        const float a = __builtin_bit_cast(float, bits);
+        double S, v, lo, hi, sl;       // S in nep units; v, lo, hi in the form's output units
+        if (which == 4) {
+            const float a1 = __builtin_amdgcn_fmed3f(a, 0.0f, qkds::kPhiHuge);
+            const qkds::PhiVal e = qkds::phi_core<true>(a1, qkds::exp_neg(a1));
+            const qkds::f2 b = qkds::phi_bounds(a, a);
+            S = a1;
+            v = e.v * 0.6931471805599453;         // psi -> phi
+            lo = b.x * 0.6931471805599453;
+            hi = b.y * 0.6931471805599453;
+            sl = e.slope;
+        } else {
+            const float at = __builtin_fminf(a, qkds::kPsiHuge);
+            const qkds::PhiVal e = qkds::phi_core<false>(at * qkds::kLn2, __builtin_amdgcn_exp2f(-at));
+            const qkds::f2 b = qkds::phi_bounds_out(a, a);
+            S = (double)at * 0.6931471805599453;
+            v = e.v;
+            lo = b.x;
+            hi = b.y;
+            sl = e.slope;
+        }
+        const double u = exp(-S);
+        const double phi = log1p(2.0 * u / -expm1(-S));            // -ln tanh(S / 2)
+        const double dphi = 2.0 * u / ((1.0 - u) * (1.0 + u));      // 1 / sinh(S)
+        ++pts;
+        bad_hi += hi < phi;
+        bad_lo += lo > phi;
+        bad_sl += sl * (1.0 + R) < dphi;
+        if (phi > 1e-30) {
+            const float err = (float)(fabs(v / phi - 1.0) / R);
+            if (err > e_max) { e_max = err; e_at = bits; }
+        }
+        const float sr = (float)(dphi / sl);
+        if (sr > s_max) { s_max = sr; s_at = bits; }
+    }
+    atomicAdd(&cnt[0], pts);
+    if (bad_hi) atomicAdd(&cnt[1], bad_hi);
+    if (bad_lo) atomicAdd(&cnt[2], bad_lo);
+    if (bad_sl) atomicAdd(&cnt[3], bad_sl);
+    sweep_max(e_max, e_at, &mx[0], &mx[2]);
+    sweep_max(s_max, s_at, &mx[1], &mx[3]);
+}
+
+qkd_status qkd_debug_phi_sweep(int which, uint32_t first_bits, uint32_t last_bits, uint64_t* result) {
+    clear_error();
+    if ((which != 4 && which != 5) || !result || first_bits > last_bits || last_bits >= 0x7f800000u)
+        return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    unsigned long long* d_cnt = nullptr;
+    uint32_t* d_mx = nullptr;
+    QKD_HIP(hipMalloc(&d_cnt, 4 * sizeof(unsigned long long)));
+    if (hipMalloc(&d_mx, 4 * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipFree(d_cnt);
+        return set_error(QKD_ERR_OUT_OF_MEMORY, "phi sweep: cannot allocate");
+    }
+    hipError_t e = hipMemset(d_cnt, 0, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_mx, 0, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(phi_sweep_kernel, dim3(4096), dim3(256), 0, nullptr, which, first_bits, last_bits, d_cnt,
+                           d_mx);
+        e = hipGetLastError();
+    }
+    unsigned long long cnt[4] = {0, 0, 0, 0};
+    uint32_t mx[4] = {0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpy(cnt, d_cnt, sizeof cnt, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(mx, d_mx, sizeof mx, hipMemcpyDeviceToHost);
+    (void)hipFree(d_cnt);
+    (void)hipFree(d_mx);
+    if (e != hipSuccess) return set_error(QKD_ERR_DEVICE, "phi sweep: %s", hipGetErrorString(e));
+    for (int k = 0; k < 4; ++k) result[k] = cnt[k];
+    for (int k = 0; k < 4; ++k) result[4 + k] = mx[k];
+    return QKD_OK;
+}
+
 qkd_status qkd_trace_decode(const qkd_code* c, const double* llr, const uint8_t* syndrome,
                             uint32_t max_iterations, double msg_threshold, uint32_t flags,
                             double* c2b_trace, double* total_trace, uint32_t* iterations,

@@ -301,3 +301,88 @@ def test_ckpt_policy_default(Q, H, golden_vectors, monkeypatch):
         torch.cuda.synchronize()
         assert (r.iterations.cpu().numpy() == golden_vectors["c3_iters"][s]).all()
         assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c3_ko"][s]).all()
+
+
+# ---- certification: exhaustive bounds, fresh frames --------------------------------
+
+F32_80 = int(np.float32(80.0).view(np.uint32))      # qkds::kPhiHuge
+F32_115 = int(np.float32(115.0).view(np.uint32))    # qkds::kPsiHuge
+
+
+@pytest.mark.parametrize("which,last", [(4, F32_80), (5, F32_115)])
+def test_phi_bounds_exhaustive(Q, which, last):
+    """EVERY positive binary32 argument up to the clamp (subnormals included, about
+    1.1e9 points per form): the upper bound is >= phi, the lower bound <= phi, and the
+    slope bound (with half its 2^-20 margin left for the tangent's own roundings) is
+    >= |phi'|, against binary64 phi on the device. With these, the bounds over any
+    [a, b] follow from phi's monotonicity and convexity (qkd_spec.h)."""
+    res = (C.c_uint64 * 8)()
+    Q._native.check(Q._native.lib().qkd_debug_phi_sweep(which, 1, last, res))
+    pts, bad_hi, bad_lo, bad_sl = res[0], res[1], res[2], res[3]
+    e_max = float(np.uint32(res[4]).view(np.float32))
+    s_max = float(np.uint32(res[5]).view(np.float32))
+    e_at = float(np.uint32(res[6]).view(np.float32))
+    s_at = float(np.uint32(res[7]).view(np.float32))
+    print(f"form {which}: {pts} points; violations hi {bad_hi} lo {bad_lo} slope {bad_sl}; "
+          f"max evaluation error {e_max:.3f} of 2^-20 at {e_at:.6g}; "
+          f"max |phi'| / slope bound {s_max:.6f} at {s_at:.6g}")
+    assert pts == last
+    assert bad_hi == 0 and bad_lo == 0 and bad_sl == 0
+    assert e_max < 0.75
+    assert s_max <= 1.0
+
+
+FRESH = 100_000
+
+
+@pytest.fixture(scope="module")
+def fresh_seeds(Q):
+    """Seeds beyond the golden vectors' first 10,000 (same stream, seed 777)."""
+    return seeds_dev(Q.make_seeds(777, 10_000 + FRESH)[10_000:])
+
+
+@pytest.mark.parametrize("q", [0.02, 0.03, 0.04, 0.05, 0.06, 0.07, 0.08])
+def test_spec_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q):
+    """100,000 frames per QBER point that no golden vector covers: the default
+    (speculative, policy-driven, run twice so the per-workspace policy settles and
+    both of its modes run) against the exact iterations alone (QKD_SPEC_CAP=0):
+    decoded words, iteration counts and flags identical."""
+    ws = Q.Workspace(H)
+    alice, bob, _ = Q.keygen(H, fresh_seeds, q, 0, workspace=ws)
+    monkeypatch.setenv("QKD_SPEC_CAP", "0")
+    ex = Q.qkd_ldpc(H, alice, bob, q, 50, 100.0, True, want_bits=True, workspace=ws)
+    monkeypatch.delenv("QKD_SPEC_CAP")
+    ws2 = Q.Workspace(H)
+    Q.spec_replays(ws2, reset=True)
+    for rep in range(2):
+        sp = Q.qkd_ldpc(H, alice, bob, q, 50, 100.0, True, want_bits=True, workspace=ws2)
+        torch.cuda.synchronize()
+        n = Q.spec_replays(ws2, reset=True)
+        assert torch.equal(sp.iterations, ex.iterations), (q, rep)
+        assert torch.equal(sp.syndromes_match, ex.syndromes_match)
+        assert torch.equal(sp.keys_match, ex.keys_match)
+        assert torch.equal(sp.bits, ex.bits), (q, rep)
+        print(f"q {q} pass {rep}: {FRESH} frames identical, {n} replayed exactly, "
+              f"mean it {ex.iterations.double().mean().item():.3f}")
+
+
+@pytest.mark.parametrize("q", [0.02, 0.05])
+def test_spec_llr_path_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q):
+    """The LLR entry (sum_product_decoding) on 100,000 fresh frames with LLRs that are
+    not +-log_p (each scaled by 1 + U(0, 0.25)): speculative = exact."""
+    ws = Q.Workspace(H)
+    alice, bob, qx = Q.keygen(H, fresh_seeds, q, 0, workspace=ws)
+    qq = float(qx[0].item())
+    lp = float(np.log((1 - qq) / qq))
+    g = torch.Generator(device="cuda").manual_seed(int(q * 1e4))
+    scale = 1.0 + 0.25 * torch.rand(bob.shape, dtype=torch.float64, device="cuda", generator=g)
+    llr = torch.where(bob == 1, -lp, lp) * scale
+    syn = Q.calculate_syndrome(H, alice)
+    monkeypatch.setenv("QKD_SPEC_CAP", "0")
+    ex = Q.sum_product_decoding(H, llr, syn, 50, 100.0, True, workspace=ws)
+    monkeypatch.delenv("QKD_SPEC_CAP")
+    sp = Q.sum_product_decoding(H, llr, syn, 50, 100.0, True, workspace=Q.Workspace(H))
+    torch.cuda.synchronize()
+    assert torch.equal(sp.iterations, ex.iterations)
+    assert torch.equal(sp.syndromes_match, ex.syndromes_match)
+    assert torch.equal(sp.bits, ex.bits)

@@ -1,57 +1,76 @@
-"""HBM-side traffic of the decode kernel per launch from rocprofv3 --pmc passes
-(tools/gpu_pmc.sh: pass 1 FETCH_SIZE, pass 2 WRITE_SIZE), corrected as
-/opt/skills/guides/MI355X_MICROARCH.md prescribes for gfx950: FETCH_SIZE (KB)
-reports 1/2 of the bytes of wide reads -> x2; WRITE_SIZE (KB) as is.
+"""Per-launch PMC record of the decode kernel from separate rocprofv3 --pmc passes
+(tools/gpu_pmc.sh), corrected as /opt/skills/guides/MI355X_MICROARCH.md prescribes
+for gfx950: FETCH_SIZE (KB) reports 1/2 of the bytes of wide reads -> x2; WRITE_SIZE
+(KB) as is.
 
-    python tools/pmc_traffic.py gpurun_out/pmc_1 gpurun_out/pmc_2 profiles/r01_pmc_decode.json [gpurun_out/pmc_3]
+    python tools/pmc_traffic.py OUT.json SUMMARY.json DIR [DIR ...]
 
-With the third directory (tools/gpu_pmc.sh pass 3: SQ_ACTIVE_INST_VALU,
-SQ_INSTS_VALU, GRBM_GUI_ACTIVE ...) the file also records the VALU busy
-fraction: SQ_ACTIVE_INST_VALU x 4 cycles / (GRBM_GUI_ACTIVE / XCDs x SIMDs).
+Every DIR holds one pass's run_counter_collection.csv. The decode kernel is the one
+dispatch name containing "decode" (the bench runs one decoder variant per pass);
+QKD_PMC_KERNEL overrides. SUMMARY.json is tools/prof_summary.py's output of the
+kernel-trace pass: the kernel's warm average duration gives the effective clock.
 """
+import collections
 import csv
 import json
 import os
 import sys
 
+N_SIMD = 1024          # 256 CUs x 4 SIMDs
+N_XCD = 8
 
-# the headline kernel: the speculative split-store decoder, keys path, binary64
-KERNEL = os.environ.get("QKD_PMC_KERNEL", "decode_split_kernel<1, 0, 6, true, 1>")
 
-
-def per_launch(d, counter):
-    vals = []
-    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            vals.append(float(r["Counter_Value"]))
-    return sum(vals) / len(vals), len(vals)
+def collect(dirs):
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in dirs:
+        for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+            per[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return per
 
 
 def main():
-    fetch_kb, nf = per_launch(sys.argv[1], "FETCH_SIZE")
-    write_kb, nw = per_launch(sys.argv[2], "WRITE_SIZE")
-    out = {
-        "kernel": KERNEL + " (qkd_qkd_ldpc_batch, 4096 frames, QBER 0.02)",
-        "fetch_size_kb": fetch_kb,
-        "write_size_kb": write_kb,
-        "launches": [nf, nw],
-        "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B",
-        "hbm_bytes_per_launch": fetch_kb * 1024 * 2 + write_kb * 1024,
-    }
-    if len(sys.argv) > 4:
-        valu, _ = per_launch(sys.argv[4], "SQ_ACTIVE_INST_VALU")
-        insts, _ = per_launch(sys.argv[4], "SQ_INSTS_VALU")
-        busy_dir = sys.argv[5] if len(sys.argv) > 5 else sys.argv[4]
-        gui, _ = per_launch(busy_dir, "GRBM_GUI_ACTIVE")
-        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles; 1024 SIMDs (256 CUs x 4)
-        cycles = gui / 8.0
-        out["valu_insts_per_launch"] = insts
-        out["valu_busy"] = valu * 4.0 / (cycles * 1024.0)
-        out["valu_note"] = ("SQ_ACTIVE_INST_VALU x 4 / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs); "
-                            "the kernel is binary64/binary32 VALU-issue bound, see DESIGN.md")
-    with open(sys.argv[3], "w") as f:
-        json.dump(out, f, indent=1)
-    print(json.dumps(out))
+    out_path, summary, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
+    per = collect(dirs)
+    want = os.environ.get("QKD_PMC_KERNEL")
+    names = [k for k in per if (want in k if want else "decode" in k)]
+    assert len(names) == 1, names
+    with open(summary) as f:
+        kernel_ms = [r["warm_avg_ms"] for r in json.load(f)["kernels"] if r["kernel"] == names[0]][0]
+    c = {k: sum(v) / len(v) for k, v in per[names[0]].items()}
+    n = {k: len(v) for k, v in per[names[0]].items()}
+    rec = {"kernel": names[0], "dispatches_per_counter": n, "counters": c,
+           "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B"}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        rec["fetch_bytes"] = c["FETCH_SIZE"] * 1024 * 2
+        rec["write_bytes"] = c["WRITE_SIZE"] * 1024
+        rec["hbm_bytes_per_launch"] = rec["fetch_bytes"] + rec["write_bytes"]
+    t = kernel_ms / 1e3
+    v = {"kernel_ms": kernel_ms}
+    if "GRBM_GUI_ACTIVE" in c:
+        cyc = c["GRBM_GUI_ACTIVE"] / N_XCD          # summed over the 8 XCDs
+        v["gpu_cycles"] = cyc
+        v["effective_clock_ghz"] = cyc / t / 1e9
+        if "SQ_INSTS_VALU" in c:
+            v["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
+            v["valu_issue_util_2cyc"] = c["SQ_INSTS_VALU"] * 2 / (cyc * N_SIMD)
+        if "SQ_ACTIVE_INST_VALU" in c:
+            v["valu_active_util_x4"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (cyc * N_SIMD)
+    if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c:
+        v["lds_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+    if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
+        v["wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+    if "SQ_WAIT_INST_LDS" in c and "SQ_WAVE_CYCLES" in c:
+        v["wait_lds_frac"] = c["SQ_WAIT_INST_LDS"] / c["SQ_WAVE_CYCLES"]
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        v["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    v["formulas"] = ("effective clock = GRBM_GUI_ACTIVE/8 / t; valu_issue_util_2cyc = SQ_INSTS_VALU x 2 "
+                     "cycles (wave64 over 32 lanes) / (cycles x 1024 SIMDs), binary64 ops take longer; "
+                     "valu_active_util_x4 = SQ_ACTIVE_INST_VALU x 4 / (cycles x 1024); lds_conflict_frac = "
+                     "SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES")
+    rec["valu"] = v
+    with open(out_path, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps({k: rec[k] for k in rec if k != "counters"}))
 
 
 if __name__ == "__main__":
