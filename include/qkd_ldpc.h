@@ -247,7 +247,8 @@ QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t 
  * [2] lower bound above phi(a), [3] slope bound (with half its 2^-20 margin)
  * below |phi'(a)|, [4] max |eval/phi - 1| / 2^-20 (binary32 bits), [5] max
  * |phi'| / slope bound (binary32 bits), [6] / [7] bit patterns where [4] / [5]
- * peak (either of the tied points). Synchronous. Test infrastructure: no
+ * peak (either of the tied points); [4]-[7] over normal a only (a subnormal a
+ * overflows the reciprocal: infinite upper bound, zero lower bound). Synchronous. Test infrastructure: no
  * reference counterpart (the reference has no speculative iterations). */
 QKD_API qkd_status qkd_debug_phi_sweep(int which, uint32_t first_bits, uint32_t last_bits, uint64_t *result);
 

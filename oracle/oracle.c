@@ -461,6 +461,37 @@ ORC_API int orc_run_trial(const orc_code *h, double q_nom, uint64_t seed, int ma
     return rc;
 }
 
+/* QKD_LDPC_interactive_simulation (simulation.cpp:73-137): ONE
+ * Xoshiro256PlusPlus(SIMULATION_SEED) (:95) feeds every QBER point in turn, each
+ * drawing Alice's key and then Bob's errors from where the previous point left
+ * the stream (:102-103). Point p's results go to slot p; errors[p] is the
+ * number of differing bits the reference prints (:115-119). Stops at the first
+ * point whose exact QBER is 0 (the reference throws there, :105-111) and
+ * returns its index, or -1 when every point ran. */
+ORC_API int orc_interactive(const orc_code *h, uint64_t sim_seed, const double *q_nom, int points,
+                            int max_it, double thr, int thr_enable, int *iters, int *sp_ok,
+                            int *key_ok, double *exact_q, int *errors) {
+    const int n = h->n;
+    orc_rng r;
+    orc_rng_seed(&r, sim_seed);
+    int *alice = (int *)malloc(sizeof(int) * (size_t)n);
+    int *bob = (int *)malloc(sizeof(int) * (size_t)n);
+    size_t *pos = (size_t *)malloc(sizeof(size_t) * (size_t)n);
+    int stop = -1;
+    for (int p = 0; p < points; p++) {
+        gen_bits(&r, n, alice);
+        double q = introduce_errors(&r, alice, n, q_nom[p], bob, pos);
+        exact_q[p] = q;
+        if (q == 0.) { stop = p; break; }
+        int e = 0;
+        for (int i = 0; i < n; i++) e += alice[i] ^ bob[i];
+        errors[p] = e;
+        orc_qkd_ldpc(h, alice, bob, q, max_it, thr, thr_enable, &iters[p], &sp_ok[p], &key_ok[p], NULL);
+    }
+    free(alice); free(bob); free(pos);
+    return stop;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Trial fan-out (the BS::thread_pool detach_loop of simulation.cpp:244-250):
  * frame k runs run_trial(seed = seeds[k] + offset) on one of `threads`

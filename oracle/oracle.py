@@ -62,6 +62,9 @@ def lib():
         L.orc_trials.restype = C.c_int
         L.orc_trials.argtypes = [P, C.c_double, u64p, C.c_uint64, C.c_size_t, C.c_int, C.c_double,
                                  C.c_int, C.c_int, i32p, i32p, i32p, f64p]
+        L.orc_interactive.restype = C.c_int
+        L.orc_interactive.argtypes = [P, C.c_uint64, f64p, C.c_int, C.c_int, C.c_double, C.c_int,
+                                      i32p, i32p, i32p, f64p, i32p]
         _lib = L
     return _lib
 
@@ -174,6 +177,22 @@ class Code:
         if rc != 0:
             raise RuntimeError(f"Key size '{self.n}' is too small for QBER.")
         return {"iters": it, "sp_ok": sp.astype(bool), "key_ok": ko.astype(bool), "exact_q": q}
+
+
+def interactive(code: "Code", sim_seed: int, q_nom, max_it=50, thr=100.0, thr_enable=True):
+    """QKD_LDPC_interactive_simulation (simulation.cpp:73-137) over the points q_nom:
+    one shared xoshiro256++ stream. Returns per-point arrays and `stop`, the index
+    of the point whose exact QBER was 0 (the reference throws there) or -1."""
+    q = np.ascontiguousarray(q_nom, dtype=np.float64)
+    p = q.size
+    it = np.zeros(p, np.int32)
+    sp = np.zeros(p, np.int32)
+    ko = np.zeros(p, np.int32)
+    ex = np.zeros(p, np.float64)
+    er = np.zeros(p, np.int32)
+    stop = lib().orc_interactive(code.h, sim_seed, q, p, max_it, thr, int(thr_enable), it, sp, ko, ex, er)
+    return {"iters": it, "sp_ok": sp.astype(bool), "key_ok": ko.astype(bool), "exact_q": ex,
+            "errors": er, "stop": int(stop)}
 
 
 def libm(which: str, x) -> np.ndarray:

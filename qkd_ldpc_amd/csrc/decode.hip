@@ -1497,19 +1497,21 @@ __global__ void phi_sweep_kernel(int which, uint32_t first, uint32_t last, unsig
             hi = b.y;
             sl = e.slope;
         }
-        const double u = exp(-S);
-        const double phi = log1p(2.0 * u / -expm1(-S));            // -ln tanh(S / 2)
-        const double dphi = 2.0 * u / ((1.0 - u) * (1.0 + u));      // 1 / sinh(S)
+        const double u = exp(-S), w = -expm1(-S);                    // e^-S, 1 - e^-S
+        const double phi = log1p(2.0 * u / w);                       // -ln tanh(S / 2)
+        const double dphi = 2.0 * u / (w * (1.0 + u));               // 1 / sinh(S)
         ++pts;
         bad_hi += hi < phi;
         bad_lo += lo > phi;
         bad_sl += sl * (1.0 + R) < dphi;
-        if (phi > 1e-30) {
+        // evaluation-error statistics over normal arguments (a subnormal a gives
+        // rcp overflow and an infinite upper bound: sound, counted above)
+        if (phi > 1e-30 && bits >= 0x00800000u) {
             const float err = (float)(fabs(v / phi - 1.0) / R);
             if (err > e_max) { e_max = err; e_at = bits; }
         }
         const float sr = (float)(dphi / sl);
-        if (sr > s_max) { s_max = sr; s_at = bits; }
+        if (sr > s_max && bits >= 0x00800000u) { s_max = sr; s_at = bits; }
     }
     atomicAdd(&cnt[0], pts);
     if (bad_hi) atomicAdd(&cnt[1], bad_hi);
