@@ -18,8 +18,13 @@
 // --gpus N (or --devices i,j,...) splits every point's trials into contiguous
 // slices, one per listed device, run concurrently and concatenated in trial
 // order, so the output does not depend on the split. --dry-run prints the
-// matrices and QBER grids and stops before any device work. Interactive mode
-// (simulation.cpp:73-137) is out of scope.
+// matrices and QBER grids and stops before any device work.
+//
+// Interactive mode (config "interactive_mode": true; main.cpp:24-27 ->
+// QKD_LDPC_interactive_simulation, simulation.cpp:73-137, select_matrix_file
+// :160-178): the same prompts, the file index read from stdin, and per QBER
+// point the reference's lines, with every point's key pair drawn from ONE
+// xoshiro256++(simulation_seed) stream (qkd_interactive_batch).
 //
 //   qkd_ldpc_sim [--root DIR] [--config FILE] [--matrix-dir DIR] [--results-dir DIR]
 //                [--gpus N | --devices i,j,...] [--variant sp_f64|sp_f32|minsum]
@@ -32,6 +37,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -316,15 +322,68 @@ Args parse_args(int argc, char** argv) {
     return a;
 }
 
+// fmt's "{}" of a double: the shortest string that reads back to the same value
+std::string shortest(double v) {
+    char buf[64];
+    const auto r = std::to_chars(buf, buf + sizeof buf, v);
+    return std::string(buf, r.ptr);
+}
+
+// QKD_LDPC_interactive_simulation (simulation.cpp:73-137) with
+// select_matrix_file (:160-178).
+int run_interactive(const Args& args, const Config& cfg, const std::vector<fs::path>& paths) {
+    std::printf("Choose file: \n");
+    for (size_t i = 0; i < paths.size(); ++i) std::printf("%zu. %s\n", i + 1, paths[i].filename().c_str());
+    std::fflush(stdout);
+    int file_index = 0;
+    std::cin >> file_index;
+    file_index -= 1;
+    if (file_index < 0 || file_index >= static_cast<int>(paths.size())) throw std::runtime_error("Wrong file number.");
+    const fs::path& path = paths[file_index];
+    const int device = args.devices.empty() ? 0 : args.devices[0];
+    qkd_status st = QKD_OK;
+    qkd_code* code = cfg.USE_DENSE_MATRICES
+                         ? qkd_code_from_dense(path.c_str(), device, &st)
+                         : qkd_code_from_alist_ex(path.c_str(), device, args.sort_rows ? QKD_READ_SORT_ROWS : 0u, &st);
+    if (!code) fail("cannot read matrix " + path.string());
+    qkd_code_info info{};
+    if (qkd_code_get_info(code, &info) != QKD_OK) fail("qkd_code_get_info");
+    std::printf("%s\n", info.is_regular ? "Matrix H is regular." : "Matrix H is irregular.");
+    const double code_rate = 1. - (static_cast<double>(info.n_checks) / info.n_bits);
+    const std::vector<double> grid = get_rate_based_QBER_range(code_rate, cfg.R_QBER_PARAMETERS);
+    const size_t P = grid.size();
+    std::vector<uint32_t> it(P), err(P);
+    std::vector<uint8_t> sp(P), ko(P);
+    std::vector<double> q(P);
+    size_t done = 0;
+    const uint32_t flags = (cfg.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD ? QKD_FLAG_THRESHOLD : 0u) | args.variant;
+    const double thr = cfg.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD ? cfg.SUM_PRODUCT_MSG_LLR_THRESHOLD : 100.0;
+    const qkd_status s = qkd_interactive_batch(code, nullptr, cfg.SIMULATION_SEED, P, grid.data(),
+                                               (uint32_t)cfg.SUM_PRODUCT_MAX_ITERATIONS, thr, flags, it.data(),
+                                               sp.data(), ko.data(), q.data(), err.data(), &done);
+    qkd_code_destroy(code);
+    for (size_t i = 0; i < done; ++i) {
+        std::printf("№:%zu\n", i + 1);
+        std::printf("Actual QBER: %s\n", shortest(q[i]).c_str());
+        std::printf("Number of errors in a key: %u\n", err[i]);
+        std::printf("Iterations performed: %u\n", it[i]);
+        std::printf("%s\n\n", (ko[i] && sp[i]) ? "Error reconciliation SUCCESSFUL" : "Error reconciliation FAILED");
+    }
+    if (s == QKD_ERR_QBER_TOO_SMALL) {
+        std::printf("№:%zu\nActual QBER: 0\n", done + 1);
+        throw std::runtime_error("Key size '" + std::to_string(info.n_bits) + "' is too small for QBER.");
+    }
+    if (s != QKD_OK) fail("qkd_interactive_batch");
+    return 0;
+}
+
 int run(int argc, char** argv) {
     const Args args = parse_args(argc, argv);
     const Config cfg = get_config_data(args.config);
-    if (cfg.INTERACTIVE_MODE)
-        throw std::runtime_error("interactive mode is not provided by this driver (batch mode only)");
     const fs::path matrix_dir = !args.matrix_dir.empty()
                                     ? args.matrix_dir
                                     : args.root / (cfg.USE_DENSE_MATRICES ? "dense_matrices" : "alist_sparse_matrices");
-    if (!args.quiet && !args.dry_run) std::printf("BATCH MODE\n");
+    if (!args.quiet && !args.dry_run) std::printf(cfg.INTERACTIVE_MODE ? "INTERACTIVE MODE\n" : "BATCH MODE\n");
     // get_file_paths_in_directory (src/utils.cpp:20-47): regular files, directory order
     if (!fs::exists(matrix_dir) || !fs::is_directory(matrix_dir)) {
         std::fprintf(stderr, "An error occurred while getting file paths in directory: %s\n", matrix_dir.c_str());
@@ -333,6 +392,7 @@ int run(int argc, char** argv) {
     std::vector<fs::path> paths;
     for (const auto& e : fs::directory_iterator(matrix_dir))
         if (fs::is_regular_file(e.path())) paths.push_back(e.path());
+    if (cfg.INTERACTIVE_MODE && !args.dry_run) return run_interactive(args, cfg, paths);
     if (paths.empty()) throw std::runtime_error("Matrix folder is empty: " + matrix_dir.string());
 
     if (args.dry_run) {

@@ -193,6 +193,22 @@ QKD_API qkd_status qkd_trials_batch(const qkd_code *code, qkd_workspace *ws, con
                             uint32_t *iterations, uint8_t *syndromes_match, uint8_t *keys_match,
                             double *exact_qber, qkd_counters *counters, void *stream);
 
+/* QKD_LDPC_interactive_simulation (simulation.cpp:73-137) over n_points
+ * nominal QBERs (host array): ONE xoshiro256++(simulation_seed) stream feeds
+ * every point's key pair in turn (:95, :102-103), then each point runs
+ * QKD_LDPC_* at its exact QBER (:122-129). Outputs are HOST arrays of
+ * n_points: iterations, syndromes_match, keys_match (the reference prints
+ * SUCCESSFUL when both hold, :131), exact_qber ("Actual QBER"), errors
+ * ("Number of errors in a key"). *points_done = points run. Like the
+ * reference, a point with floor(N*q) == 0 stops the run there and returns
+ * QKD_ERR_QBER_TOO_SMALL with the earlier points' results filled in.
+ * Synchronous (device-synchronising); ws may be NULL. */
+QKD_API qkd_status qkd_interactive_batch(const qkd_code *code, qkd_workspace *ws, uint64_t simulation_seed,
+                                         size_t n_points, const double *q_nominal, uint32_t max_iterations,
+                                         double msg_threshold, uint32_t flags, uint32_t *iterations,
+                                         uint8_t *syndromes_match, uint8_t *keys_match, double *exact_qber,
+                                         uint32_t *errors, size_t *points_done);
+
 /* Reduction alone: per-frame results -> counters (device memory). */
 QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t *syndromes_match,
                               const uint8_t *keys_match, size_t n_frames, qkd_counters *counters,

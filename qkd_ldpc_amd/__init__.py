@@ -15,6 +15,7 @@ src/array_and_matrix_operations.hpp) with batched, device-resident arrays:
   run_trial over a batch + the batch reduction    run_trials(H, seeds, q_nominal, ...)
   seeds of QKD_LDPC_batch_simulation              make_seeds(simulation_seed, count)
   get_rate_based_QBER_range (one table row)       qber_range(begin, end, step)
+  QKD_LDPC_interactive_simulation                 interactive_simulation(H, seed, qbers, ...)
 
 Errors surface as QkdError (a RuntimeError, as the reference throws
 std::runtime_error). Every call runs HIP kernels; nothing falls back to CPU.
@@ -39,7 +40,7 @@ __all__ = [
     "sum_product_decoding_irregular", "sum_product_decoding_regular", "qkd_ldpc",
     "QKD_LDPC_irregular", "QKD_LDPC_regular", "keygen", "run_trials", "make_seeds",
     "qber_range", "Workspace", "counters_to_stats", "decoder_flags", "trace_decode",
-    "spec_replays",
+    "spec_replays", "interactive_simulation",
 ]
 
 
@@ -361,6 +362,38 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                                      _ptr(out.iterations), _ptr(out.syndromes_match),
                                      _ptr(out.keys_match), _ptr(out.exact_qber),
                                      _ptr(out.counters), _stream(stream, H.device)))
+    return out
+
+
+def interactive_simulation(H: HMatrix, simulation_seed: int, qbers, max_iterations: int = 50,
+                           msg_threshold: float = 100.0, threshold_enabled: bool = True,
+                           workspace=None, variant: str = "sp_f64") -> dict:
+    """QKD_LDPC_interactive_simulation (simulation.cpp:73-137): the QBER points share ONE
+    xoshiro256++(simulation_seed) key stream, point after point. Returns host arrays per
+    point: exact_qber ("Actual QBER"), errors, iterations, syndromes_match, keys_match,
+    success (both flags, "Error reconciliation SUCCESSFUL"). A point whose exact QBER
+    would be 0 raises QkdError like the reference's throw; the points before it ran."""
+    q = np.ascontiguousarray(qbers, dtype=np.float64)
+    p = q.size
+    it = np.zeros(p, np.uint32)
+    sp = np.zeros(p, np.uint8)
+    ko = np.zeros(p, np.uint8)
+    ex = np.zeros(p, np.float64)
+    er = np.zeros(p, np.uint32)
+    done = C.c_size_t(0)
+    st = N.lib().qkd_interactive_batch(H.handle, _ws(workspace), simulation_seed, p, q.ctypes.data,
+                                       max_iterations, msg_threshold,
+                                       decoder_flags(threshold_enabled, variant), it.ctypes.data,
+                                       sp.ctypes.data, ko.ctypes.data, ex.ctypes.data, er.ctypes.data,
+                                       C.byref(done))
+    k = done.value
+    out = {"points_done": k, "exact_qber": ex[:k], "errors": er[:k], "iterations": it[:k],
+           "syndromes_match": sp[:k].astype(bool), "keys_match": ko[:k].astype(bool),
+           "success": (sp[:k] & ko[:k]).astype(bool)}
+    if st != N.OK:
+        err = QkdError(st, N.last_error())
+        err.partial = out
+        raise err
     return out
 
 

@@ -1416,6 +1416,111 @@ qkd_status qkd_keygen_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t
     return QKD_OK;
 }
 
+// ---- interactive mode: one key stream across the QBER points ------------------
+// QKD_LDPC_interactive_simulation (simulation.cpp:73-137) seeds ONE
+// Xoshiro256PlusPlus(SIMULATION_SEED) (:95) and draws every point's Alice key
+// and Bob errors from it in turn (:102-103), so point p starts where point p-1's
+// shuffle stopped, Lemire rejections included. A handful of points per run and
+// no throughput target: one thread walks the stream exactly as the reference
+// does (the batch path's jump-ahead keygen needs independent seeds).
+__global__ void keygen_stream_kernel(uint64_t sim_seed, uint32_t n, uint32_t words, uint32_t n_points,
+                                     const uint32_t* ne, uint64_t* alice_w, uint64_t* bob_w, uint32_t* low) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    qkdr::Xoshiro256pp g;
+    g.seed(sim_seed);
+    for (uint32_t p = 0; p < n_points; ++p) {
+        uint64_t* A = alice_w + (size_t)p * words;
+        uint64_t* B = bob_w + (size_t)p * words;
+        for (uint32_t w = 0; w < words; ++w) {
+            const uint32_t nb = min(64u, n - w * 64);
+            uint64_t v = 0;
+            for (uint32_t b = 0; b < nb; ++b) v |= (g.next() >> 63) << b;
+            A[w] = v;
+            B[w] = v;
+        }
+        qkdr::shuffle_low_positions(g, n, ne[p], low);
+        for (uint32_t k = 0; k < ne[p]; ++k) B[low[k] >> 6] ^= 1ull << (low[k] & 63);
+    }
+}
+
+qkd_status qkd_interactive_batch(const qkd_code* c, qkd_workspace* ws, uint64_t simulation_seed, size_t n_points,
+                                 const double* q_nominal, uint32_t max_iterations, double msg_threshold,
+                                 uint32_t flags, uint32_t* iterations, uint8_t* syndromes_match,
+                                 uint8_t* keys_match, double* exact_qber, uint32_t* errors, size_t* points_done) {
+    clear_error();
+    if (!c || !q_nominal || !iterations || !syndromes_match || !keys_match || !exact_qber || !errors || !points_done)
+        return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    *points_done = 0;
+    if (n_points == 0 || n_points > (1u << 20)) return set_error(QKD_ERR_INVALID_ARG, "bad point count");
+    qkd_status s = check_decode_params(max_iterations, msg_threshold, flags);
+    if (s != QKD_OK) return s;
+    // the reference throws at the first point whose exact QBER is 0 (:105-111),
+    // after running the points before it
+    std::vector<uint32_t> ne;
+    uint32_t max_ne = 1;
+    size_t run = n_points;
+    for (size_t p = 0; p < n_points; ++p) {
+        if (!(q_nominal[p] > 0.0 && q_nominal[p] <= 1.0)) return set_error(QKD_ERR_INVALID_ARG, "QBER must be in (0,1]");
+        const uint64_t e = qkdr::num_errors((uint32_t)c->n, q_nominal[p]);
+        if (e == 0) {
+            run = p;
+            break;
+        }
+        ne.push_back((uint32_t)e);
+        max_ne = std::max(max_ne, (uint32_t)e);
+    }
+    DeviceGuard g(c->device);
+    ws = resolve_ws(c, ws);
+    if (!ws) return set_error(QKD_ERR_OUT_OF_MEMORY, "no workspace");
+    hipStream_t st = nullptr;
+    if (run > 0) {
+        WsSession sess(ws, st);
+        s = ws_reserve_keys(ws, 1, 1);
+        if (s != QKD_OK) return s;
+        const uint32_t words = (uint32_t)((c->n + 63) / 64);
+        uint64_t *d_a = nullptr, *d_b = nullptr;
+        uint32_t *d_ne = nullptr, *d_low = nullptr, *d_it = nullptr;
+        uint8_t* d_flags = nullptr;
+        auto cleanup = [&]() {
+            for (void* q : {(void*)d_a, (void*)d_b, (void*)d_ne, (void*)d_low, (void*)d_it, (void*)d_flags})
+                if (q) (void)hipFree(q);
+        };
+        if (hipMalloc(&d_a, run * words * 8) != hipSuccess || hipMalloc(&d_b, run * words * 8) != hipSuccess ||
+            hipMalloc(&d_ne, run * 4) != hipSuccess || hipMalloc(&d_low, (size_t)max_ne * 4) != hipSuccess ||
+            hipMalloc(&d_it, run * 4) != hipSuccess || hipMalloc(&d_flags, run * 2) != hipSuccess) {
+            cleanup();
+            return set_error(QKD_ERR_OUT_OF_MEMORY, "interactive: cannot allocate");
+        }
+        hipError_t e = hipMemcpy(d_ne, ne.data(), run * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(keygen_stream_kernel, dim3(1), dim3(64), 0, st, simulation_seed, (uint32_t)c->n, words,
+                               (uint32_t)run, d_ne, d_a, d_b, d_low);
+            e = hipGetLastError();
+        }
+        for (size_t p = 0; p < run && e == hipSuccess && s == QKD_OK; ++p) {
+            exact_qber[p] = (double)ne[p] / (double)c->n;
+            errors[p] = ne[p];   // distinct positions: every flip is a differing bit (:115-119)
+            e = hipMemcpyAsync(ws->alice_w, d_a + p * words, words * 8, hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(ws->bob_w, d_b + p * words, words * 8, hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess)
+                s = decode_keys(c, ws, 1, exact_qber[p], max_iterations, msg_threshold, flags, nullptr, d_it + p,
+                                d_flags + p, d_flags + run + p, st);
+        }
+        if (e == hipSuccess && s == QKD_OK) e = hipMemcpy(iterations, d_it, run * 4, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && s == QKD_OK) e = hipMemcpy(syndromes_match, d_flags, run, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && s == QKD_OK) e = hipMemcpy(keys_match, d_flags + run, run, hipMemcpyDeviceToHost);
+        cleanup();
+        if (s != QKD_OK) return s;
+        if (e != hipSuccess) return set_error(QKD_ERR_DEVICE, "interactive: %s", hipGetErrorString(e));
+    }
+    *points_done = run;
+    if (run < n_points) {
+        exact_qber[run] = 0.0;
+        return set_error(QKD_ERR_QBER_TOO_SMALL, "Key size '%d' is too small for QBER.", c->n);
+    }
+    return QKD_OK;
+}
+
 __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

@@ -138,9 +138,7 @@ def test_matrix_directory_errors(sim_bin, tmp_path, golden_code):
     os.rmdir(root / "alist_sparse_matrices")
     r = run(sim_bin, root, "--dry-run")
     assert r.returncode == 1 and "Directory doesn't exist." in r.stderr
-    cfg = dict(BASE_CFG, interactive_mode=True)
-    r = run(sim_bin, make_root(tmp_path, golden_code, cfg), "--dry-run")
-    assert r.returncode == 1 and "interactive mode" in r.stderr
+
 
 
 def test_dry_run_grids_match_reference_rule(sim_bin, tmp_path, golden_code, dense_codes):
@@ -220,3 +218,77 @@ def test_batch_run_csv_equals_oracle(sim_bin, tmp_path, golden_code, oracle_mod,
     assert r2.returncode == 0, r2.stderr
     second = root / "results" / name.replace(").csv", ")_1.csv")
     assert second.read_text(encoding="utf-8") == text      # split over three shards: same rows
+
+
+# ---- interactive mode (simulation.cpp:73-137) ------------------------------------------
+
+INTERACTIVE_CFG = dict(BASE_CFG, interactive_mode=True, code_rate_QBER_parameters=[
+    {"code_rate": 0.58, "QBER_begin": 0.06, "QBER_end": 0.0745, "QBER_step": 0.0005}])   # config.json:20-23
+
+
+def interactive_lines(res, n_points):
+    """The lines QKD_LDPC_interactive_simulation prints per point (:100-132)."""
+    out = []
+    for i in range(n_points):
+        out += [f"№:{i + 1}", f"Actual QBER: {res['exact_q'][i]!r}",
+                f"Number of errors in a key: {res['errors'][i]}",
+                f"Iterations performed: {res['iters'][i]}",
+                "Error reconciliation SUCCESSFUL" if res["sp_ok"][i] and res["key_ok"][i]
+                else "Error reconciliation FAILED"]
+    return out
+
+
+def test_interactive_rejects_bad_file_number(sim_bin, tmp_path, golden_code):
+    root = make_root(tmp_path, golden_code, INTERACTIVE_CFG)
+    r = subprocess.run([sim_bin, "--root", str(root)], input="7\n", capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1 and "Wrong file number." in r.stderr
+    assert "INTERACTIVE MODE" in r.stdout and f"1. {ALIST_NAME}" in r.stdout
+
+
+@pytest.mark.gpu
+def test_interactive_driver_matches_oracle(sim_bin, tmp_path, golden_code, oracle_code, oracle_mod):
+    """The reference's default grid for the R=0.49 code (30 points, QBER 0.06-0.0745)
+    with one shared key stream: every printed line equals the oracle's restatement."""
+    root = make_root(tmp_path, golden_code, INTERACTIVE_CFG)
+    r = subprocess.run([sim_bin, "--root", str(root)], input="1\n", capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rate = 1 - 5231 / 10240
+    grid = ref_grid(rate, INTERACTIVE_CFG["code_rate_QBER_parameters"])
+    assert len(grid) == 29
+    want = oracle_mod.interactive(oracle_code, 777, grid, 50, 100.0, True)
+    assert want["stop"] == -1
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert lines[:3] == ["INTERACTIVE MODE", "Choose file: ", f"1. {ALIST_NAME}"]
+    assert lines[3] == "Matrix H is irregular."
+    assert lines[4:] == interactive_lines(want, len(grid))
+
+
+@pytest.mark.gpu
+def test_interactive_api_and_too_small_qber(golden_code, oracle_code, oracle_mod, dense_codes):
+    """qkd_interactive_batch through Python: per-point results equal the oracle's,
+    the stream continues across points (point 2 differs from a fresh seed), and a
+    point with floor(N q) = 0 stops the run there with the earlier points done."""
+    import qkd_ldpc_amd as Q
+    g = golden_code
+    H = Q.HMatrix.from_check_lists(10240, g["chk_off"], g["chk_idx"])
+    qs = [0.02, 0.05, 0.08, 0.03, 0.11]
+    got = Q.interactive_simulation(H, 12345, qs)
+    want = oracle_mod.interactive(oracle_code, 12345, qs)
+    for k in ("iterations", "errors"):
+        assert got[k].tolist() == want["iters" if k == "iterations" else k].tolist(), k
+    assert got["syndromes_match"].tolist() == want["sp_ok"].tolist()
+    assert got["keys_match"].tolist() == want["key_ok"].tolist()
+    assert got["exact_qber"].tolist() == want["exact_q"].tolist()
+    # the dense N=10 code: 0.05 * 10 floors to 0 at the third point
+    name = "(N=10,K=5,M=5,R=0.5).txt"
+    Hd = Q.HMatrix.from_dense_array(dense_codes[name])
+    od = oracle_mod.Code.from_dense(dense_codes[name])
+    qd = [0.2, 0.1, 0.05, 0.3]
+    want = oracle_mod.interactive(od, 777, qd, 100, 100.0, True)
+    assert want["stop"] == 2
+    with pytest.raises(Q.QkdError) as ei:
+        Q.interactive_simulation(Hd, 777, qd, 100)
+    part = ei.value.partial
+    assert ei.value.status == Q._native.ERR_QBER_TOO_SMALL and part["points_done"] == 2
+    assert part["iterations"].tolist() == want["iters"][:2].tolist()
+    assert part["success"].tolist() == (want["sp_ok"] & want["key_ok"])[:2].tolist()
