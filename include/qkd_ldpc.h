@@ -69,8 +69,10 @@ typedef enum qkd_status {
  * frame error rates are compared with the reference's, not their frames. */
 #define QKD_VARIANT_MASK   0x30u
 #define QKD_VARIANT_SP_F64 0x00u  /* sum-product, binary64 (the reference)    */
-#define QKD_VARIANT_SP_F32 0x10u  /* sum-product, binary32, OCML tanhf/atanhf;
-                                     |P/t| limited to 1 - 2^-24             */
+#define QKD_VARIANT_SP_F32 0x10u  /* sum-product, binary32, Gallager form:
+                                     c2b = sign * phi(sum of the other
+                                     phi(|b2c|)), phi(x) = -ln tanh(x/2),
+                                     hardware exp2/log2                      */
 #define QKD_VARIANT_MINSUM 0x20u  /* normalised min-sum, binary32:
                                      c2b = scale * sign * min |b2c| over the
                                      check's other edges                     */
@@ -79,6 +81,10 @@ typedef enum qkd_status {
 #define QKD_MINSUM_SCALE_SHIFT 8
 #define QKD_MINSUM_SCALE(x) ((((uint32_t)((x) * 256.0 + 0.5)) & 0xffu) << QKD_MINSUM_SCALE_SHIFT)
 #define QKD_MINSUM_DEFAULT_SCALE 0.8125  /* best FER of {0.625..0.875} on config 3 */
+/* Min-sum offset in flag bits 16-23 as round(offset * 64): the message magnitude
+ * is max(scale * min |b2c| - offset, 0) (offset min-sum); 0 = no offset. */
+#define QKD_MINSUM_OFFSET_SHIFT 16
+#define QKD_MINSUM_OFFSET(x) ((((uint32_t)((x) * 64.0 + 0.5)) & 0xffu) << QKD_MINSUM_OFFSET_SHIFT)
 
 typedef struct qkd_code qkd_code;
 typedef struct qkd_workspace qkd_workspace;
@@ -248,7 +254,8 @@ QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, con
 /* The decoder's tanh (which = 0) / atanh (which = 1) restatement applied to
  * x[n] -> y[n] (device arrays): the bit-exactness check of the device build
  * against glibc (reference qkd_ldpc_algorithm.cpp:224, :241). which = 2 / 3:
- * the binary32 variant's tanh(x/2) / 2*atanh(x) (QKD_VARIANT_SP_F32), x
+ * the binary32 variant's two transcendental steps (QKD_VARIANT_SP_F32): the
+ * published sign(x) * phi(|x|) / ln 2 and phi(S ln 2) of a psi-unit sum S, x
  * rounded to binary32, result widened. which = 4 / 5: certified bounds of
  * phi(x) = -ln tanh(x/2) over [x[2k], x[2k+1]] (the speculative iterations'
  * input / output forms, qkd_spec.h) -> y[2k] = lower, y[2k+1] = upper; n even;
@@ -263,8 +270,10 @@ QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t 
  * [2] lower bound above phi(a), [3] slope bound (with half its 2^-20 margin)
  * below |phi'(a)|, [4] max |eval/phi - 1| / 2^-20 (binary32 bits), [5] max
  * |phi'| / slope bound (binary32 bits), [6] / [7] bit patterns where [4] / [5]
- * peak (either of the tied points); [4]-[7] over normal a only (a subnormal a
- * overflows the reciprocal: infinite upper bound, zero lower bound). Synchronous. Test infrastructure: no
+ * peak (either of the tied points); [4]-[7] over normal a with a finite
+ * evaluation only (a subnormal argument overflows the reciprocal: infinite
+ * upper bound, zero lower bound; the kernel never feeds such an argument to
+ * the output form, whose sums are at least phi(80) / ln 2). Synchronous. Test infrastructure: no
  * reference counterpart (the reference has no speculative iterations). */
 QKD_API qkd_status qkd_debug_phi_sweep(int which, uint32_t first_bits, uint32_t last_bits, uint64_t *result);
 

@@ -8,8 +8,9 @@ operation rounds exactly as the kernel's does:
 
   schedule      the reference's flooding loop (qkd_ldpc_algorithm.cpp:212-330)
   b2c           LLR_i at iteration 0 (:188), else clamp(total_i - c2b) (:303-316)
-  c2b           scale * (-1)^(s_j + #negative other b2c) * min over the other |b2c|
-                (NaN inputs ignored by the min, as fminf), then clamp (:246-249)
+  c2b           (-1)^(s_j + #negative other b2c) * max(scale * min over the other
+                |b2c| - offset, 0) (offset 0: plain normalised min-sum; NaN inputs
+                ignored by the min, as fminf), then clamp (:246-249)
   total         float(LLR_i) + c2b_0 + c2b_1 + ... in ascending check order (:256-267)
   stop          H z == s, z_i = total_i <= 0 (:277-285)
 """
@@ -55,7 +56,7 @@ class MinSumModel:
     def _clamp(v, thr):
         return np.where(v > thr, thr, np.where(v < -thr, -thr, v)).astype(np.float32)
 
-    def decode(self, llr, syndrome, max_it=50, thr=100.0, thr_enable=True, scale=0.8125):
+    def decode(self, llr, syndrome, max_it=50, thr=100.0, thr_enable=True, scale=0.8125, offset=0.0):
         """llr [F, N] float64, syndrome [F, M] -> (bits [F, N] u8, iterations [F], sp_ok [F])."""
         llr32 = np.asarray(llr, np.float64).astype(np.float32)
         syn = np.asarray(syndrome, np.uint8)
@@ -86,6 +87,8 @@ class MinSumModel:
                 mn = np.fmin.reduce(others, axis=2) if others.shape[2] else np.full(mag.shape[:2], np.inf, np.float32)
                 mn = mn.astype(np.float32)
                 v = (sc * mn).astype(np.float32)
+                if offset > 0:
+                    v = np.fmax((v - np.float32(offset)).astype(np.float32), np.float32(0))
                 neg = neg_all ^ negb[:, :, k]
                 v = np.where(neg == 1, -v, v).astype(np.float32)
                 if thr_enable:
@@ -112,16 +115,35 @@ class MinSumModel:
         return out_bits, iters, ok
 
 
+def _psi_np(x):
+    """Signed psi(|x|) = sign(x) phi(|x|) / ln 2 in numpy (|x| limited to [1e-30, 80]):
+    the statistical stand-in for the device's evaluation (qkd_debug_math which = 2)."""
+    a = np.abs(np.asarray(x, np.float32)).astype(np.float64)
+    a = np.where(a < 1e-30, 1e-30, np.where(a > 80.0, 80.0, a))
+    p = np.log1p(2 * np.exp(-a) / -np.expm1(-a)) / np.log(2.0)
+    return np.where(np.asarray(x) < 0, -p, p).astype(np.float32)
+
+
+def _phi_out_np(s):
+    """phi(S ln 2) of a psi-unit sum S (limited to 115): stand-in for which = 3."""
+    S = np.minimum(np.asarray(s, np.float64), 115.0) * np.log(2.0)
+    with np.errstate(divide="ignore"):
+        return np.log1p(2 * np.exp(-S) / -np.expm1(-S)).astype(np.float32)
+
+
 def sp_f32_decode(model: MinSumModel, llr, syndrome, max_it=50, thr=100.0, thr_enable=True,
                   trace=None, tanh_half=None, two_atanh=None, trace_ref=None):
-    """Model of QKD_VARIANT_SP_F32 -> (bits, iterations, sp_ok). With the device's own
-    elementwise tanh(x/2) / 2 atanh(x) plugged in (qkd_debug_math which = 2 / 3) it is
-    the kernel's specification bit for bit; with numpy's float32 tanh / arctanh
-    (the default) it tracks the kernel statistically.
+    """Model of QKD_VARIANT_SP_F32 -> (bits, iterations, sp_ok): binary32 messages and
+    totals, the check rule in Gallager's form (qkd_decode.h RuleMath<kRuleSp32>):
+      p_k  = sign(b2c_k) psi(|b2c_k|)                       (published per edge)
+      S    = sum over the other edges of |p_m|, ascending    (binary32 adds)
+      c2b  = (-1)^(s_j + #negative other p) phi(S ln 2), clamped
+    With the device's own elementwise steps plugged in (tanh_half = the published
+    value, qkd_debug_math which = 2; two_atanh = phi(S ln 2), which = 3) it is the
+    kernel's specification bit for bit; with the numpy stand-ins (the default) it
+    tracks the kernel statistically.
     trace: optional list; per iteration it receives (n_nan_messages, n_zero_b2c, n_errors
-    of the hard decision vs trace_ref if given). tanh_half / two_atanh: optional
-    replacements of the two transcendental steps (e.g. the device's, through
-    qkd_debug_math) taking and returning float32 arrays."""
+    of the hard decision vs trace_ref if given)."""
     llr32 = np.asarray(llr, np.float64).astype(np.float32)
     syn = np.asarray(syndrome, np.uint8)
     F = llr32.shape[0]
@@ -141,22 +163,20 @@ def sp_f32_decode(model: MinSumModel, llr, syndrome, max_it=50, thr=100.0, thr_e
                 b2c = (b2c - c2b).astype(np.float32)
                 if thr_enable:
                     b2c = MinSumModel._clamp(b2c, thr32)
-            t = (tanh_half(b2c) if tanh_half else np.tanh(b2c * np.float32(0.5))).astype(np.float32)
-            T = t[:, cs]
-            sgn = np.where(syn == 1, np.float32(-1), np.float32(1)).astype(np.float32)
+            pub = (tanh_half(b2c) if tanh_half else _psi_np(b2c)).astype(np.float32)
+            P = pub[:, cs]
             new = np.zeros_like(c2b)
             for k in range(model.dc):
-                # extrinsic product over the other edges, ascending, no division
-                r = sgn.copy()
+                # extrinsic psi sum over the other edges, ascending, and their sign parity
+                S = np.zeros(P.shape[:2], np.float32)
+                neg = syn.astype(np.uint8).copy()
                 for j in range(model.dc):
                     if j != k:
-                        r = np.where(valid[None, :, j], (r * T[:, :, j]).astype(np.float32), r)
-                if two_atanh:
-                    v = two_atanh(r).astype(np.float32)
-                else:
-                    kmax = np.float32(np.nextafter(np.float32(1), np.float32(0)))
-                    r = np.where(r > kmax, kmax, np.where(r < -kmax, -kmax, r))
-                    v = (np.float32(2) * np.arctanh(r)).astype(np.float32)
+                        on = valid[None, :, j]
+                        S = np.where(on, (S + np.abs(P[:, :, j])).astype(np.float32), S)
+                        neg = np.where(on, neg ^ (P[:, :, j] < 0).astype(np.uint8), neg)
+                v = (two_atanh(S) if two_atanh else _phi_out_np(S)).astype(np.float32)
+                v = np.where(neg == 1, -v, v).astype(np.float32)
                 if thr_enable:
                     v = MinSumModel._clamp(v, thr32)
                 col = valid[:, k]

@@ -45,7 +45,7 @@ __all__ = [
 
 
 def decoder_flags(threshold_enabled: bool = True, variant: str = "sp_f64",
-                  minsum_scale: float | None = None) -> int:
+                  minsum_scale: float | None = None, minsum_offset: float | None = None) -> int:
     """Flag word of the decode entry points: the reference's threshold switch
     (CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD) and the check-node rule:
     "sp_f64" (the reference, bit-exact), "sp_f32" or "minsum" (build-defined
@@ -60,6 +60,13 @@ def decoder_flags(threshold_enabled: bool = True, variant: str = "sp_f64",
         if not (1 <= q <= 255) or q != minsum_scale * 256:
             raise ValueError("minsum_scale must be k/256 for k in 1..255")
         flags |= q << N.MINSUM_SCALE_SHIFT
+    if minsum_offset is not None:
+        if variant != "minsum":
+            raise ValueError("minsum_offset applies to variant='minsum' only")
+        q = round(minsum_offset * 64)
+        if not (0 <= q <= 255) or q != minsum_offset * 64:
+            raise ValueError("minsum_offset must be k/64 for k in 0..255")
+        flags |= q << N.MINSUM_OFFSET_SHIFT
     return flags
 
 
@@ -256,7 +263,8 @@ class LDPCResult:
 def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
                          msg_threshold: float = 100.0, threshold_enabled: bool = True,
                          want_bits: bool = True, workspace=None, stream=None,
-                         variant: str = "sp_f64", minsum_scale: float | None = None) -> SPResult:
+                         variant: str = "sp_f64", minsum_scale: float | None = None,
+                         minsum_offset: float | None = None) -> SPResult:
     """sum_product_decoding_irregular/_regular (qkd_ldpc_algorithm.cpp:3-345), batched.
     llr [F, N] float64, syndrome [F, M] uint8 (0/1)."""
     _need_cuda(llr, torch.float64, "llr", H)
@@ -267,7 +275,7 @@ def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
     bits = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev) if want_bits else None
     iters = torch.empty(f, dtype=torch.int32, device=dev)
     ok = torch.empty(f, dtype=torch.uint8, device=dev)
-    flags = decoder_flags(threshold_enabled, variant, minsum_scale)
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset)
     N.check(N.lib().qkd_decode_batch(H.handle, _ws(workspace), _ptr(llr), _ptr(syndrome), f,
                                      max_iterations, msg_threshold, flags, _ptr(bits), _ptr(iters),
                                      _ptr(ok), _stream(stream, H.device)))
@@ -282,7 +290,8 @@ sum_product_decoding_regular = sum_product_decoding
 def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
              msg_threshold: float = 100.0, threshold_enabled: bool = True,
              want_bits: bool = False, workspace=None, stream=None,
-             variant: str = "sp_f64", minsum_scale: float | None = None) -> LDPCResult:
+             variant: str = "sp_f64", minsum_scale: float | None = None,
+             minsum_offset: float | None = None) -> LDPCResult:
     """QKD_LDPC_irregular/_regular (qkd_ldpc_algorithm.cpp:347-447), batched.
     alice, bob [F, N] uint8 (0/1); one QBER for the batch."""
     _need_cuda(alice, torch.uint8, "alice", H)
@@ -294,7 +303,7 @@ def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
     iters = torch.empty(f, dtype=torch.int32, device=dev)
     ok = torch.empty(f, dtype=torch.uint8, device=dev)
     km = torch.empty(f, dtype=torch.uint8, device=dev)
-    flags = decoder_flags(threshold_enabled, variant, minsum_scale)
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset)
     N.check(N.lib().qkd_qkd_ldpc_batch(H.handle, _ws(workspace), _ptr(alice), _ptr(bob), f, qber,
                                        max_iterations, msg_threshold, flags, _ptr(bits),
                                        _ptr(iters), _ptr(ok), _ptr(km), _stream(stream, H.device)))
@@ -335,7 +344,7 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                max_iterations: int = 50, msg_threshold: float = 100.0,
                threshold_enabled: bool = True, workspace=None, stream=None,
                out: TrialResults | None = None, variant: str = "sp_f64",
-               minsum_scale: float | None = None) -> TrialResults:
+               minsum_scale: float | None = None, minsum_offset: float | None = None) -> TrialResults:
     """run_trial (simulation.cpp:161-189) for every frame, fused on the device, plus the
     per-QBER-point counters of simulation.cpp:252-312. seeds: int64 CUDA tensor holding
     the uint64 seed bits."""
@@ -356,7 +365,7 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                            torch.empty(f, dtype=torch.uint8, device=dev),
                            torch.empty(f, dtype=torch.float64, device=dev),
                            torch.empty(N.COUNTERS_BYTES, dtype=torch.uint8, device=dev))
-    flags = decoder_flags(threshold_enabled, variant, minsum_scale)
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset)
     N.check(N.lib().qkd_trials_batch(H.handle, _ws(workspace), _ptr(seeds), seed_offset, f,
                                      q_nominal, max_iterations, msg_threshold, flags,
                                      _ptr(out.iterations), _ptr(out.syndromes_match),

@@ -39,6 +39,7 @@ READ_SORT_ROWS = 0x1   # qkd_code_from_alist_ex
 # decoder variants (include/qkd_ldpc.h: QKD_VARIANT_*)
 VARIANTS = {"sp_f64": 0x00, "sp_f32": 0x10, "minsum": 0x20}
 MINSUM_SCALE_SHIFT = 8
+MINSUM_OFFSET_SHIFT = 16
 MINSUM_DEFAULT_SCALE = 0.8125
 
 # Every symbol include/qkd_ldpc.h declares (checked by tests/test_abi.py).

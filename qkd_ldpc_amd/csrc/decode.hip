@@ -66,7 +66,7 @@ template <int SRC, bool CLAMP, int DC, int RULE, typename T>
 __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
                                             const T* total, const uint16_t* t2idx, const double* tab2,
                                             T* __restrict__ c2b, T* row, int n_tasks, int n_pad, T thr,
-                                            int wave, int lane, float ms_scale) {
+                                            int wave, int lane, float ms_scale, float ms_offset) {
     constexpr int NW = kDecodeBlock / 64;
     constexpr bool FIRST = SRC != kSrcGeneral;    // no stored message is read
     int t = wave;
@@ -87,7 +87,7 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
         const T a = edge_in<SRC, CLAMP, RULE>(x, o, thr);
         row[lane] = a;
         wave_lds_sync();
-        return edge_out<CLAMP, DC, RULE>(a, w, sbit(w), lane, thr, row, ms_scale);
+        return edge_out<CLAMP, DC, RULE>(a, w, sbit(w), lane, thr, row, ms_scale, ms_offset);
     };
     uint2 wa = pl[t * 64];
     uint2 wb = pl[(t + NW) * 64];
@@ -134,9 +134,10 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
 // totals (n * 4 B) stay in LDS, and the decode touches no global memory but
 // the code's own (L2-resident) arrays.
 template <bool CLAMP>
-__device__ __forceinline__ float ms_msg(uint4 st, uint32_t pos, float scale, float thr) {
+__device__ __forceinline__ float ms_msg(uint4 st, uint32_t pos, float scale, float off, float thr) {
     const float m = pos == (st.w & 0xffu) ? __uint_as_float(st.y) : __uint_as_float(st.x);
     float v = scale * m;
+    if (off > 0.0f) v = fmaxf(v - off, 0.0f);
     const uint32_t neg = (st.w >> 31) ^ ((st.z >> pos) & 1u);
     v = neg ? -v : v;
     if (CLAMP) v = clamp_msg(v, thr);
@@ -156,7 +157,7 @@ __device__ __forceinline__ float ms_msg(uint4 st, uint32_t pos, float scale, flo
 //   state = (min |b2c|, second min, argmin, signs, s_j ^ parity)
 template <int SRC, bool CLAMP, int DC>
 __device__ __forceinline__ void ms_check_phase(const DeviceCode& c, const uint32_t* tsyn, const float* total,
-                                               uint4* cst, float thr, float scale) {
+                                               uint4* cst, float thr, float scale, float off) {
     const int m = c.m;
     int j = threadIdx.x;
     if (j >= m) return;
@@ -181,7 +182,7 @@ __device__ __forceinline__ void ms_check_phase(const DeviceCode& c, const uint32
             if (bl[k] >= 0) {
                 float x = total[bl[k]];
                 if (SRC == kSrcGeneral) {
-                    x = x - ms_msg<CLAMP>(st, (uint32_t)k, scale, thr);
+                    x = x - ms_msg<CLAMP>(st, (uint32_t)k, scale, off, thr);
                     if (CLAMP) x = clamp_msg(x, thr);
                 }
                 const float a = fabsf(x);
@@ -422,9 +423,9 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             if constexpr (MSL) {
                 tabled = true;
                 if (it == 0)
-                    ms_check_phase<kSrcFirst, CLAMP, DC>(c, tsyn, total, cst, thr, a.ms_scale);
+                    ms_check_phase<kSrcFirst, CLAMP, DC>(c, tsyn, total, cst, thr, a.ms_scale, a.ms_offset);
                 else
-                    ms_check_phase<kSrcGeneral, CLAMP, DC>(c, tsyn, total, cst, thr, a.ms_scale);
+                    ms_check_phase<kSrcGeneral, CLAMP, DC>(c, tsyn, total, cst, thr, a.ms_scale, a.ms_offset);
             }
             if constexpr (TABLES) {
                 tabled = true;
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     first_check_phase(plan, tsyn, total, ctab, c2b, n_tasks, n_pad, wave, lane);
                 else if (it == 1 && a.tab2_entries)
                     check_phase<kSrcTable, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks,
-                                                            n_pad, thr, wave, lane, a.ms_scale);
+                                                            n_pad, thr, wave, lane, a.ms_scale, a.ms_offset);
                 else
                     tabled = false;
             }
@@ -442,10 +443,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                 if (!tabled) {
                     if (it == 0)
                         check_phase<kSrcFirst, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row, n_tasks,
-                                                                n_pad, thr, wave, lane, a.ms_scale);
+                                                                n_pad, thr, wave, lane, a.ms_scale, a.ms_offset);
                     else
                         check_phase<kSrcGeneral, CLAMP, DC, RULE>(plan, tsyn, total, t2idx, tab2, c2b, row,
-                                                                  n_tasks, n_pad, thr, wave, lane, a.ms_scale);
+                                                                  n_tasks, n_pad, thr, wave, lane, a.ms_scale, a.ms_offset);
                 }
             }
             __syncthreads();
@@ -506,14 +507,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
                     if constexpr (MSL) {
 #pragma unroll
                         for (int k = 0; k < kDvUnroll; ++k)
-                            if (k < deg) v[u][k] = ms_msg<CLAMP>(cst[jc[u][k]], ps[u][k], a.ms_scale, thr);
+                            if (k < deg) v[u][k] = ms_msg<CLAMP>(cst[jc[u][k]], ps[u][k], a.ms_scale, a.ms_offset, thr);
                     }
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
                     if constexpr (MSL) {
                         for (int k = kDvUnroll; k < deg; ++k)
                             acc = acc + ms_msg<CLAMP>(cst[c.bit_chk[k * n_pad + i]], c.bit_pos[k * n_pad + i],
-                                                      a.ms_scale, thr);
+                                                      a.ms_scale, a.ms_offset, thr);
                     } else {
                         for (int k = kDvUnroll; k < deg; ++k) acc = acc + c2b[k * n_pad + i];
                     }
@@ -1040,6 +1041,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     const bool ms_global = ms_store && !strcmp(ms_store, "global");
     if (rule == kRuleMinSum && !ms_global && decode_ms_fits(c)) rule = kRuleMinSumLds;
     a.ms_scale = minsum_scale_of(flags);
+    a.ms_offset = (float)((flags >> QKD_MINSUM_OFFSET_SHIFT) & 0xffu) / 64.0f;
     // The split-store kernel (decode_split.hip) for the sum-product rules
     // whenever its LDS layout fits; QKD_DECODE_KERNEL=classic keeps
     // decode_kernel (A/B measurements, tests). Trace mode records the classic
@@ -1160,12 +1162,13 @@ static qkd_status check_frames(size_t n_frames) {
 
 static qkd_status check_decode_params(uint32_t max_it, double thr, uint32_t flags) {
     if (max_it < 1) return set_error(QKD_ERR_INVALID_ARG, "max_iterations must be >= 1");
-    const uint32_t known = QKD_FLAG_THRESHOLD | QKD_VARIANT_MASK | (0xffu << QKD_MINSUM_SCALE_SHIFT);
+    const uint32_t known = QKD_FLAG_THRESHOLD | QKD_VARIANT_MASK | (0xffu << QKD_MINSUM_SCALE_SHIFT) |
+                           (0xffu << QKD_MINSUM_OFFSET_SHIFT);
     if (flags & ~known) return set_error(QKD_ERR_INVALID_ARG, "unknown flags 0x%x", flags);
     if ((flags & QKD_VARIANT_MASK) == QKD_VARIANT_MASK)
         return set_error(QKD_ERR_INVALID_ARG, "unknown decoder variant 0x%x", flags & QKD_VARIANT_MASK);
     if ((flags >> QKD_MINSUM_SCALE_SHIFT) && (flags & QKD_VARIANT_MASK) != QKD_VARIANT_MINSUM)
-        return set_error(QKD_ERR_INVALID_ARG, "min-sum scale given without QKD_VARIANT_MINSUM");
+        return set_error(QKD_ERR_INVALID_ARG, "min-sum scale or offset given without QKD_VARIANT_MINSUM");
     if ((flags & QKD_FLAG_THRESHOLD) && !(thr > 0.0))
         return set_error(QKD_ERR_INVALID_ARG, "message threshold must be > 0");
     return QKD_OK;
@@ -1271,7 +1274,10 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     a.words = (uint32_t)((c->n + 63) / 64);
     a.log_p = std::log((1. - q) / q);          // host glibc log, qkd_ldpc_algorithm.cpp:400
     // first-iteration message magnitudes by check degree (first_check_phase)
-    a.first_table = (c->max_dc <= kFirstTableDeg && rule_of(flags) == kRuleSp64) ? 1 : 0;
+    // (the binary32 rule folds on the device, decode_split_kernel; not at
+    // log_p = 0, where Bob's 1 bits give -0.0, not negative)
+    a.first_table = (c->max_dc <= kFirstTableDeg &&
+                     (rule_of(flags) == kRuleSp64 || (rule_of(flags) == kRuleSp32 && a.log_p != 0.0))) ? 1 : 0;
     if (a.first_table) {
         const double T = std::fabs(qkdm::tanh_flat(a.log_p / 2.0));
         double M = 1.0;
@@ -1283,7 +1289,8 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
             a.first_c2b[d] = v;
         }
     }
-    a.tab2_entries = (a.first_table && c->n_pat > 0) ? c->n_pat * tab2_stride(c->max_dv) : 0;
+    a.tab2_entries = (a.first_table && c->n_pat > 0 && rule_of(flags) == kRuleSp64)
+                         ? c->n_pat * tab2_stride(c->max_dv) : 0;
     // speculative interval iterations (decode_split.hip, qkd_spec.h) ahead of
     // the exact ones, for the binary64 rule with clamped messages;
     // QKD_SPEC_CAP overrides how many (0: off)
@@ -1527,7 +1534,7 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
     switch (which) {
         case 0: y[i] = qkdm::tanh_flat(x[i]); break;
         case 1: y[i] = qkdm::atanh_flat(x[i]); break;
-        case 2: y[i] = (double)RuleMath<kRuleSp32>::tanh_half((float)x[i]); break;
+        case 2: y[i] = (double)RuleMath<kRuleSp32>::tanh_half((float)x[i]); break;   // signed psi(|x|)
         case 4:
         case 5: {
             // phi bounds over [x[2k], x[2k+1]] -> y[2k] = lo, y[2k+1] = hi
@@ -1549,7 +1556,7 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
         }
         case 6: y[i] = (double)__builtin_amdgcn_exp2f((float)x[i]); break;   // hardware v_exp_f32
         case 7: y[i] = (double)__builtin_amdgcn_logf((float)x[i]); break;    // hardware v_log_f32
-        default: y[i] = (double)RuleMath<kRuleSp32>::two_atanh((float)x[i]); break;
+        default: y[i] = (double)RuleMath<kRuleSp32>::two_atanh((float)x[i]); break;  // phi(S ln 2)
     }
 }
 
@@ -1611,7 +1618,7 @@ __global__ void phi_sweep_kernel(int which, uint32_t first, uint32_t last, unsig
         bad_sl += sl * (1.0 + R) < dphi;
         // evaluation-error statistics over normal arguments (a subnormal a gives
         // rcp overflow and an infinite upper bound: sound, counted above)
-        if (phi > 1e-30 && bits >= 0x00800000u) {
+        if (phi > 1e-30 && bits >= 0x00800000u && v < 3.0e38) {
             const float err = (float)(fabs(v / phi - 1.0) / R);
             if (err > e_max) { e_max = err; e_at = bits; }
         }

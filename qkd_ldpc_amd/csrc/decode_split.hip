@@ -390,6 +390,10 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
 template <int MODE, int RULE, int DC, bool CLAMP, int SPEC>
 __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a) {
     using T = typename RuleMsg<RULE>::T;
+    // QKD path: the first check phase folds into the first bit phase for both
+    // sum-product rules (every b2c is +-log_p, so every message is +-C_d:
+    // ctab); the second-iteration tanh table is the binary64 rule's only
+    constexpr bool FOLDS = MODE == kModeKeys && (RULE == kRuleSp64 || RULE == kRuleSp32);
     constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
@@ -419,7 +423,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;     // sign bit of log_p
     // the first check phase is folded into the first bit phase (QKD path;
     // the fold rebuilds the unrolled rows only)
-    const bool fold1 = TABLES && a.first_table && c.max_dv <= kDvUnroll;
+    const bool fold1 = FOLDS && a.first_table && c.max_dv <= kDvUnroll;
     const bool tab2_on = fold1 && a.tab2_entries;
     uint32_t rnd = 0;    // rounds (iterations of any frame) run by this workgroup
     if (tid == 0) { ctl[2] = 0; ctl[3] = 0; ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
@@ -431,6 +435,19 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
 #endif
     constexpr int BC = SPEC ? kBitChunkSpec : QKD_EXACT_CHUNK;      // exact bit phase load batch
     if (TABLES && tid <= kFirstTableDeg) ctab[tid] = a.first_c2b[tid];
+    if constexpr (RULE == kRuleSp32 && FOLDS) {
+        // the binary32 rule's first messages by check degree d, evaluated exactly
+        // as split_check_phase would on d inputs of equal magnitude |float(log_p)|:
+        // S = ((0 + p) + p) + ... over the d - 1 other edges, C_d = phi(S ln 2)
+        if (tid <= kFirstTableDeg) {
+            const float p = __builtin_fabsf(RuleMath<kRuleSp32>::tanh_half((float)a.log_p));
+            float S = 0.0f;
+            for (int k = 1; k < tid; ++k) S = S + p;
+            float v = RuleMath<kRuleSp32>::two_atanh(S);
+            if (CLAMP) v = clamp_msg(v, (float)a.thr);
+            ctab[tid] = (double)v;
+        }
+    }
     if (tab2_on) {
         __syncthreads();
         second_table_fill<CLAMP>(c, ctab, a.log_p, a.thr, tab2, a.tab2_entries);
@@ -567,7 +584,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                                                                    wave, lane);
                 __syncthreads();
             }
-            pc.mark((TABLES && it < 2 && fold1) ? 5 + (int)it : 1);
+            pc.mark((FOLDS && it < 2 && fold1) ? 5 + (int)it : 1);
             // the b2c of this bit phase are read only by a next iteration
             const bool keep = it + 1 < a.max_it;
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
@@ -616,7 +633,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     T acc;
                     if (MODE == kModeLlr) acc = ok ? (T)a.llr[(size_t)f * c.n + i] : (T)0;
                     else acc = ((bobmask >> r) & 1u) ? -llr_p : llr_p;
-                    if constexpr (TABLES) if (folded && ok) {
+                    if constexpr (FOLDS) if (folded && ok) {
                         // fold_first_message: message of the k-th check j of bit i is
                         // +-C_{d_j} with sign = sign(P_j) ^ sign(LLR_i) (first_check_phase)
                         const uint32_t sgi = ((bobmask >> r) & 1u) ^ lsign;
@@ -625,7 +642,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                             if (k < deg) {
                                 const int j = jc[u][k];
                                 const uint32_t sp = (qsyn[j >> 5] >> (j & 31)) & 1u;
-                                const double cm = ctab[c.chk_deg[j]];
+                                const T cm = (T)ctab[c.chk_deg[j]];
                                 v[u][k] = (sp ^ sgi) ? -cm : cm;
                             }
                         }

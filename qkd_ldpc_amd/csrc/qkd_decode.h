@@ -8,6 +8,7 @@
 #include "qkd_internal.h"
 #include "qkd_math.h"
 #include "qkd_plan.h"
+#include "qkd_spec.h"
 
 namespace qkd {
 
@@ -34,8 +35,9 @@ enum DecodeMode : int {
 
 // Check-node rule and message width (QKD_VARIANT_* in qkd_ldpc.h).
 //   kRuleSp64   the reference's sum-product in binary64, bit-exact
-//   kRuleSp32   the same schedule with binary32 messages and totals, OCML
-//               tanhf/atanhf (a variant: not bit-exact to anything)
+//   kRuleSp32   the same schedule with binary32 messages and totals, the
+//               check rule in Gallager's form with the hardware exp2 / log2
+//               (a variant: not bit-exact to anything)
 //   kRuleMinSum normalised min-sum in binary32: c2b = scale * sign * min|b2c|
 //               over the other edges of the check (a variant, no transcendental)
 //   kRuleMinSumLds  the same min-sum with the frame's whole message state in
@@ -52,6 +54,7 @@ struct DecodeArgs {
     double thr;
     int clamp_on;
     float ms_scale;    // kRuleMinSum normalisation
+    float ms_offset;   // kRuleMinSum offset (subtracted after the scale, floored at 0)
     // kModeLlr
     const double* llr;
     const uint8_t* syn;
@@ -252,17 +255,26 @@ template <> struct RuleMath<kRuleSp64> {
     static __device__ __forceinline__ double tanh_half(double x) { return qkdm::tanh_flat(x / 2.0); }
     static __device__ __forceinline__ double two_atanh(double p) { return 2.0 * qkdm::atanh_flat(p); }
 };
+// The binary32 variant evaluates the check rule in Gallager's form,
+//   c2b = sigma * phi(sum_{k != self} phi(|b2c_k|)),  phi(x) = -ln tanh(x / 2),
+// sigma = s_j xor the other signs: the sum-product rule without the tanh
+// domain's binary32 trouble (tanh(b2c / 2) rounds to 1 from |b2c| ~ 18 on,
+// and P / t is 0 / 0 when a b2c cancels to 0). "tanh_half" publishes
+// sign(b2c) * psi(|b2c|), psi = phi / ln 2 (qkds::phi_core, hardware
+// v_exp_f32 / v_log_f32), with |b2c| limited to [1e-30, 80] so psi is finite
+// and positive (the sign survives); "two_atanh" maps a psi-unit sum S to
+// phi(S ln 2) (qkds::phi_bounds_out's evaluation, S limited to 115).
 template <> struct RuleMath<kRuleSp32> {
-    static __device__ __forceinline__ float tanh_half(float x) { return tanhf(x * 0.5f); }
-    // In binary32, tanh(b2c / 2) rounds to 1 from |b2c| ~ 18 on, so the
-    // extrinsic ratio P / t lands on (or one ulp beyond) +-1 far more often
-    // than in binary64, and 2 atanh(+-1) = +-inf would turn a ~17 message into
-    // the clamp value. The ratio is therefore limited to the largest binary32
-    // below 1 (|message| <= 2 atanh(1 - 2^-24) = 17.33); NaN (0/0) still passes.
-    static __device__ __forceinline__ float two_atanh(float p) {
-        constexpr float kMax = 0x1.fffffep-1f;
-        p = p > kMax ? kMax : (p < -kMax ? -kMax : p);
-        return 2.0f * atanhf(p);
+    static __device__ __forceinline__ float tanh_half(float x) {
+        float a = __builtin_fabsf(x);
+        a = a < 1.0e-30f ? 1.0e-30f : a;
+        a = a > qkds::kPhiHuge ? qkds::kPhiHuge : a;
+        const float p = qkds::phi_core<true>(a, qkds::exp_neg(a)).v;
+        return x < 0.0f ? -p : p;
+    }
+    static __device__ __forceinline__ float two_atanh(float s) {
+        const float at = s > qkds::kPsiHuge ? qkds::kPsiHuge : s;
+        return qkds::phi_core<false>(at * qkds::kLn2, __builtin_amdgcn_exp2f(-at)).v;
     }
 };
 
@@ -297,7 +309,7 @@ __device__ __forceinline__ T edge_in(T x, T old, T thr) {
 // past a segment's end stay inside it and are discarded).
 template <bool CLAMP, int DC, int RULE, typename T>
 __device__ __forceinline__ T edge_out(T tv, uint2 w, uint32_t sbit, int lane, T thr, const T* row,
-                                      float ms_scale) {
+                                      float ms_scale, float ms_offset = 0.0f) {
     const int start = pw_start(w);
     const int deg = pw_deg(w);
     T o[DC];
@@ -316,6 +328,7 @@ __device__ __forceinline__ T edge_out(T tv, uint2 w, uint32_t sbit, int lane, T 
             }
         }
         v = (T)ms_scale * mn;
+        if (ms_offset > 0.0f) v = fmaxf(v - (T)ms_offset, (T)0);
         v = neg ? -v : v;
     } else if constexpr (RULE == kRuleSp64) {
         // the reference's P = (s_j ? -1 : 1) * prod_k t_k, then 2 atanh(P / t_self) (:231-241)
@@ -325,14 +338,19 @@ __device__ __forceinline__ T edge_out(T tv, uint2 w, uint32_t sbit, int lane, T 
         for (int k = 1; k < DC; ++k) P = k < deg ? P * o[k] : P;
         v = RuleMath<RULE>::two_atanh(P / tv);
     } else {
-        // binary32 variant: the extrinsic product over the other edges in
-        // ascending order, no division. (P / t is 0/0 = NaN when b2c is
-        // exactly 0, which binary32 cancellation makes a ~1 % per-frame
-        // event at QBER 0.05, and the NaN then floods the frame.)
-        T P = sbit ? (T)-1 : (T)1;
+        // binary32 variant (Gallager form, RuleMath<kRuleSp32>): the extrinsic
+        // psi sum over the other edges in ascending order and their sign parity
+        T S = (T)0;
+        uint32_t neg = sbit;
 #pragma unroll
-        for (int k = 0; k < DC; ++k) P = (k < deg && start + k != lane) ? P * o[k] : P;
-        v = RuleMath<RULE>::two_atanh(P);
+        for (int k = 0; k < DC; ++k) {
+            if (k < deg && start + k != lane) {
+                S = S + __builtin_fabsf(o[k]);
+                neg ^= o[k] < (T)0 ? 1u : 0u;
+            }
+        }
+        v = RuleMath<RULE>::two_atanh(S);
+        v = neg ? -v : v;
     }
     if (CLAMP) v = clamp_msg(v, thr);
     return v;

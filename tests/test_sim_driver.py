@@ -230,7 +230,7 @@ def interactive_lines(res, n_points):
     """The lines QKD_LDPC_interactive_simulation prints per point (:100-132)."""
     out = []
     for i in range(n_points):
-        out += [f"№:{i + 1}", f"Actual QBER: {res['exact_q'][i]!r}",
+        out += [f"№:{i + 1}", f"Actual QBER: {float(res['exact_q'][i])!r}",
                 f"Number of errors in a key: {res['errors'][i]}",
                 f"Iterations performed: {res['iters'][i]}",
                 "Error reconciliation SUCCESSFUL" if res["sp_ok"][i] and res["key_ok"][i]

@@ -329,7 +329,7 @@ def test_phi_bounds_exhaustive(Q, which, last):
     assert pts == last
     assert bad_hi == 0 and bad_lo == 0 and bad_sl == 0
     assert e_max < 0.75
-    assert s_max <= 1.0
+    assert s_max <= 1.0 + 2.0 ** -21          # the slope bound's own margin is 2^-20
 
 
 FRESH = 100_000

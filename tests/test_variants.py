@@ -89,19 +89,22 @@ def _dev(x, dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("q,max_it,thr,thr_on,scale", [
-    (0.02, 50, 100.0, True, None),
-    (0.06, 50, 100.0, True, None),
-    (0.08, 50, 100.0, True, 0.8125),
-    (0.08, 7, 2.5, True, 0.5),
-    (0.05, 50, 0.0, False, None),
-    (0.10, 3, 0.7, True, 255 / 256),
+@pytest.mark.parametrize("q,max_it,thr,thr_on,scale,offset", [
+    (0.02, 50, 100.0, True, None, None),
+    (0.06, 50, 100.0, True, None, None),
+    (0.08, 50, 100.0, True, 0.8125, None),
+    (0.08, 7, 2.5, True, 0.5, None),
+    (0.05, 50, 0.0, False, None, None),
+    (0.10, 3, 0.7, True, 255 / 256, None),
+    (0.08, 50, 100.0, True, 0.9375, 0.25),
+    (0.07, 50, 2.5, True, 1.0 - 1 / 256, 3.0),
 ])
 @pytest.mark.parametrize("store", ["lds", "global"])
 def test_minsum_llr_bit_exact(Q, H, ms_model, oracle_mod, monkeypatch, store, q, max_it, thr, thr_on,
-                              scale):
+                              scale, offset):
     """Both min-sum kernels: the frame state in LDS (per-check min1/min2/argmin/
-    signs, the default where it fits) and the per-edge global message store."""
+    signs, the default where it fits) and the per-edge global message store; plain
+    normalised and offset min-sum."""
     if store == "global":
         monkeypatch.setenv("QKD_MINSUM_STORE", "global")
     A, B, qq = _frames(oracle_mod, q, 48, seed=int(q * 1000) + max_it)
@@ -110,10 +113,10 @@ def test_minsum_llr_bit_exact(Q, H, ms_model, oracle_mod, monkeypatch, store, q,
     syn = ms_model.syndrome(A)
     r = Q.sum_product_decoding(H, _dev(llr, np.float64), _dev(syn, np.uint8), max_it,
                                thr if thr_on else 100.0, thr_on, variant="minsum",
-                               minsum_scale=scale)
+                               minsum_scale=scale, minsum_offset=offset)
     torch.cuda.synchronize()
     want_bits, want_it, want_ok = ms_model.decode(llr, syn, max_it, thr, thr_on,
-                                                  0.8125 if scale is None else scale)
+                                                  0.8125 if scale is None else scale, offset or 0.0)
     assert (r.iterations.cpu().numpy() == want_it).all()
     assert (r.syndromes_match.cpu().numpy() == want_ok).all()
     assert (r.bits.cpu().numpy() == want_bits).all()
@@ -172,17 +175,25 @@ def _dev_math(which):
 
 @pytest.mark.gpu
 def test_sp_f32_elementwise_math_close_to_numpy(Q):
-    from qkd_ldpc_amd import _native as N
-    x = np.concatenate([np.linspace(-100, 100, 20001), np.linspace(-1, 1, 20001), [0.0, -0.0, 1.0, -1.0]])
-    kmax = np.float32(np.nextafter(np.float32(1), np.float32(0)))
+    """The binary32 variant's two steps (Gallager form) against binary64 numpy: the
+    published sign(x) psi(|x|) and phi(S ln 2)."""
+    from oracle.variants import _phi_out_np, _psi_np
+    # binary32 arguments (the device rounds its inputs to binary32; phi(x) ~ 2 e^-x
+    # turns an argument rounding into a relative error of x 2^-24)
+    x = np.concatenate([np.linspace(-100, 100, 20001), np.geomspace(1e-12, 1, 20001),
+                        -np.geomspace(1e-12, 1, 2001), [0.0, -0.0, 1.0, -1.0, 80.0, 1e-30]])
+    s = np.concatenate([np.geomspace(1e-30, 200, 40001), [0.0]])
+    x = x.astype(np.float32).astype(np.float64)
+    s = s.astype(np.float32).astype(np.float64)
     with np.errstate(all="ignore"):
-        th = _dev_math(2)(x)
-        at = _dev_math(3)(x)
-        want_th = np.tanh(x.astype(np.float32) * np.float32(0.5))
-        want_at = np.float32(2) * np.arctanh(np.clip(x.astype(np.float32), -kmax, kmax))
-    assert np.allclose(th, want_th, rtol=4e-7, atol=0)
-    assert np.allclose(at, want_at, rtol=4e-7, atol=0)
-    assert np.abs(at).max() <= np.float32(17.33)
+        pub = _dev_math(2)(x)
+        out = _dev_math(3)(s)
+    want_pub, want_out = _psi_np(x), _phi_out_np(s)
+    assert (np.sign(pub[x != 0]) == np.sign(x[x != 0])).all()
+    assert np.allclose(pub, want_pub, rtol=2e-6, atol=0)
+    fin = np.isfinite(want_out)
+    assert np.allclose(out[fin], want_out[fin], rtol=2e-6, atol=1e-37)
+    assert np.isinf(out[~fin]).all()
 
 
 @pytest.mark.gpu
@@ -205,10 +216,31 @@ def test_sp_f32_bit_exact_with_device_math(Q, H, ms_model, oracle_mod, q, max_it
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("q,max_it,thr", [(0.03, 50, 100.0), (0.08, 50, 100.0), (0.06, 2, 3.0), (0.07, 1, 100.0)])
+def test_sp_f32_keys_path_bit_exact(Q, H, ms_model, oracle_mod, q, max_it, thr):
+    """qkd_ldpc with the binary32 rule: its first check phase is folded into the first
+    bit phase (messages +-C_d from a per-degree table the kernel evaluates with the same
+    device steps), so the keys path must equal the unfolded specification bit for bit."""
+    from oracle.variants import sp_f32_decode
+    A, B, qq = _frames(oracle_mod, q, 24, seed=int(q * 1000) + max_it)
+    r = Q.qkd_ldpc(H, _dev(A, np.uint8), _dev(B, np.uint8), float(qq), max_it, thr, True,
+                   want_bits=True, variant="sp_f32")
+    torch.cuda.synchronize()
+    lp = np.log((1 - qq) / qq)
+    llr = np.where(B == 1, -lp, lp)
+    wb, wi, wo = sp_f32_decode(ms_model, llr, ms_model.syndrome(A), max_it, thr, True,
+                               tanh_half=_dev_math(2), two_atanh=_dev_math(3))
+    assert (r.iterations.cpu().numpy() == wi).all()
+    assert (r.syndromes_match.cpu().numpy() == wo).all()
+    assert (r.bits.cpu().numpy() == wb).all()
+    assert (r.keys_match.cpu().numpy() == (wb == A).all(axis=1)).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("q", [0.02, 0.05])
 def test_sp_f32_tracks_reference(Q, H, q):
-    """binary32 sum-product: where the code has margin it decodes every frame,
-    and to the same iteration count as the reference decoder on nearly all."""
+    """binary32 sum-product (Gallager form): where the code has margin it decodes every
+    frame, and to the same iteration count as the reference decoder on nearly all."""
     seeds = torch.from_numpy(Q.make_seeds(777, 1024).view(np.int64)).cuda()
     ref = Q.run_trials(H, seeds, q)
     f32 = Q.run_trials(H, seeds, q, variant="sp_f32")
