@@ -263,12 +263,18 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
 #define QKD_IV_CHUNK 3
 #endif
 constexpr int kIvChunk = QKD_IV_CHUNK;       // rounds per load batch
-template <bool FOLD, int MODE>
+// DV3: every bit has exactly kDvUnroll (3) checks (a column-weight-3 code,
+// like the reference's N = 10240 one): no per-degree guards, so the round is
+// straight-line code except one branch around the hard decision's syndrome
+// updates (and a rare one around the uncertainty marks). The general form
+// guards every row by the bit's degree.
+template <bool FOLD, int MODE, bool DV3>
 __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const DecodeArgs& a, const SplitStore<double>& ms,
                                                const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
                                                uint32_t* xunc, uint64_t* zw, uint32_t bobmask, bool keep,
                                                uint32_t f, int tid, int wave, int lane) {
     using qkds::f2;
+    static_assert(!DV3 || kDvUnroll == 3, "DV3 unrolls three rows");
     const uint32_t n_pad = (uint32_t)c.n_pad;
     const double llr_p = a.log_p;
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
@@ -291,8 +297,10 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             if (r * kDecodeBlock >= c.n) break;            // block-uniform
             const int i = tid + r * kDecodeBlock;
             const uint32_t iw = (uint32_t)(r * kDecodeBlock + wave * 64);
-            const bool ok = i < c.n;
-            const int deg = (int)(bc[u] >> 48) & 3;
+            // a full round (block-uniform): every lane's bit exists
+            const bool full = (r + 1) * kDecodeBlock <= c.n;
+            const bool ok = full || i < c.n;
+            const int deg = DV3 ? kDvUnroll : (int)(bc[u] >> 48) & 3;
             int32_t jc[kDvUnroll];
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k) jc[k] = (int32_t)(bc[u] >> (16 * k)) & 0xffff;
@@ -306,16 +314,13 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 double cv[kDvUnroll];
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) {
-                    cv[k] = 0.0;
-                    if (k < deg) {
-                        const int j = jc[k];
-                        const uint32_t sp = (qsyn[j >> 5] >> (j & 31)) & 1u;
-                        const double cm = ctab[((uint32_t)(bc[u] >> (50 + 4 * k)) & 15u) + 1u];
-                        cv[k] = (sp ^ sgi) ? -cm : cm;
-                    }
+                    const int j = jc[k];
+                    const uint32_t sp = (qsyn[j >> 5] >> (j & 31)) & 1u;
+                    const double cm = ctab[((uint32_t)(bc[u] >> (50 + 4 * k)) & 15u) + 1u];
+                    cv[k] = (DV3 || k < deg) ? ((sp ^ sgi) ? -cm : cm) : 0.0;
                 }
 #pragma unroll
-                for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + cv[k] : acc;
+                for (int k = 0; k < kDvUnroll; ++k) acc = (DV3 || k < deg) ? acc + cv[k] : acc;
                 z = ok && acc <= 0;
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) bo[k] = qkds::iv_of(clamp_msg(acc - cv[k], a.thr));
@@ -328,7 +333,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 float mag = __builtin_fmaxf(__builtin_fabsf(L.x), __builtin_fabsf(L.y));
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) {
-                    cs[k] = k < deg ? qkds::unpack_iv(v[u][k]) : f2{0.0f, 0.0f};
+                    cs[k] = (DV3 || k < deg) ? qkds::unpack_iv(v[u][k]) : f2{0.0f, 0.0f};
                     T = T + cs[k];
                     mag = mag + __builtin_fmaxf(__builtin_fabsf(cs[k].x), __builtin_fabsf(cs[k].y));
                 }
@@ -357,17 +362,23 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             if (z) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
-                    if (k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
+                    if (DV3 || k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
             }
             if (unc) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
-                    if (k < deg) atomicOr(&xunc[jc[k] >> 5], 1u << (jc[k] & 31));
+                    if (DV3 || k < deg) atomicOr(&xunc[jc[k] >> 5], 1u << (jc[k] & 31));
             }
-            if (!keep || !ok) continue;
+            if (!keep) continue;
+            if (DV3 && full) {
 #pragma unroll
-            for (int k = 0; k < kDvUnroll; ++k)
-                if (k < deg) ms.st_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i, qkds::pack_iv(bo[k]));
+                for (int k = 0; k < kDvUnroll; ++k)
+                    ms.st_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i, qkds::pack_iv(bo[k]));
+            } else if (ok) {
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k)
+                    if (k < deg) ms.st_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i, qkds::pack_iv(bo[k]));
+            }
         }
     }
 }
@@ -424,6 +435,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     // the first check phase is folded into the first bit phase (QKD path;
     // the fold rebuilds the unrolled rows only)
     const bool fold1 = FOLDS && a.first_table && c.max_dv <= kDvUnroll;
+    // column weight 3 throughout (the speculative bit phase's straight-line form)
+    const bool dv3 = c.min_dv == kDvUnroll && c.max_dv == kDvUnroll;
     const bool tab2_on = fold1 && a.tab2_entries;
     uint32_t rnd = 0;    // rounds (iterations of any frame) run by this workgroup
     if (tid == 0) { ctl[2] = 0; ctl[3] = 0; ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
@@ -592,12 +605,21 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // then b2c_k = clamp(total_i - c2b_k) (:303-316) into slot k.
             if (SPEC && spec) {
                 if constexpr (SPEC) {
-                    if (folded)
-                        spec_bit_phase<true, MODE>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, f, tid,
-                                                   wave, lane);
-                    else
-                        spec_bit_phase<false, MODE>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep, f, tid,
-                                                    wave, lane);
+                    if (dv3) {
+                        if (folded)
+                            spec_bit_phase<true, MODE, true>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
+                                                             f, tid, wave, lane);
+                        else
+                            spec_bit_phase<false, MODE, true>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
+                                                              f, tid, wave, lane);
+                    } else {
+                        if (folded)
+                            spec_bit_phase<true, MODE, false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
+                                                              f, tid, wave, lane);
+                        else
+                            spec_bit_phase<false, MODE, false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
+                                                               f, tid, wave, lane);
+                    }
                 }
             } else
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += BC) {

@@ -104,6 +104,7 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     c->min_dc = max_dc;
     for (int32_t j = 0; j < m; ++j) c->min_dc = std::min(c->min_dc, cptr[j + 1] - cptr[j]);
     c->max_dv = max_dv;
+    c->min_dv = *std::min_element(bdeg.begin(), bdeg.end());
     c->check_ptr.assign(cptr, cptr + m + 1);
     c->check_idx.assign(cidx, cidx + e);
     // bit side: iterate checks ascending -> each bit row ascending

@@ -46,6 +46,7 @@ struct DeviceCode {
     int32_t n, m, e;
     int32_t n_pad, m_pad;
     int32_t max_dv, max_dc, min_dc;
+    int32_t min_dv;
     int32_t n_tasks;
     const int32_t* chk_bits;
     const uint8_t* chk_deg;
@@ -108,7 +109,7 @@ struct qkd_workspace {
 struct qkd_code {
     int device = 0;
     int32_t n = 0, m = 0, e = 0;
-    int32_t max_dv = 0, max_dc = 0, min_dc = 0, is_regular = 0;
+    int32_t max_dv = 0, max_dc = 0, min_dc = 0, min_dv = 0, is_regular = 0;
     int32_t n_pad = 0, m_pad = 0;
     int32_t n_tasks = 0;
     std::vector<int32_t> check_ptr, check_idx, bit_ptr, bit_idx;
@@ -131,7 +132,7 @@ struct qkd_code {
     qkd_workspace* default_ws = nullptr;
 
     qkd::DeviceCode view() const {
-        return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, n_tasks,
+        return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
                                n_pat, d_bit_pat, d_pat_deg, d_bit_code};
     }
