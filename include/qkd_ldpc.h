@@ -259,7 +259,10 @@ QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, con
  * rounded to binary32, result widened. which = 4 / 5: certified bounds of
  * phi(x) = -ln tanh(x/2) over [x[2k], x[2k+1]] (the speculative iterations'
  * input / output forms, qkd_spec.h) -> y[2k] = lower, y[2k+1] = upper; n even;
- * which = 5 takes its interval in log2-domain units (x = S / ln 2). */
+ * which = 5 takes its interval in log2-domain units (x = S / ln 2).
+ * which = 8 / 9: quadruples (a, b, s_lo, s_hi) -> raw binary32 (in lo, in hi,
+ * out lo, out hi) of the packed phi_pair (8) and of the scalar phi_bounds +
+ * phi_bounds_out it must equal bit for bit (9); n a multiple of 4. */
 QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
 /* Exhaustive check of the speculative iterations' phi bounds (qkd_spec.h) at
  * EVERY binary32 a with bit pattern in [first_bits, last_bits] (positive

@@ -1554,6 +1554,25 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
             }
             break;
         }
+        case 8:
+        case 9: {
+            // quadruples (a, b, s_lo, s_hi) -> (in lo, in hi, out lo, out hi),
+            // raw binary32 results: 8 the packed qkds::phi_pair, 9 the scalar
+            // phi_bounds (psi units) and phi_bounds_out; one thread per quadruple
+            if (i & 3) break;
+            qkds::f2 in, out;
+            if (which == 8) {
+                qkds::phi_pair((float)x[i], (float)x[i + 1], (float)x[i + 2], (float)x[i + 3], in, out);
+            } else {
+                in = qkds::phi_bounds((float)x[i], (float)x[i + 1]);
+                out = qkds::phi_bounds_out((float)x[i + 2], (float)x[i + 3]);
+            }
+            y[i] = in.x;
+            y[i + 1] = in.y;
+            y[i + 2] = out.x;
+            y[i + 3] = out.y;
+            break;
+        }
         case 6: y[i] = (double)__builtin_amdgcn_exp2f((float)x[i]); break;   // hardware v_exp_f32
         case 7: y[i] = (double)__builtin_amdgcn_logf((float)x[i]); break;    // hardware v_log_f32
         default: y[i] = (double)RuleMath<kRuleSp32>::two_atanh((float)x[i]); break;  // phi(S ln 2)
@@ -1562,8 +1581,10 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
 
 qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void* stream) {
     clear_error();
-    if (!x || !y || which < 0 || which > 7) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if (!x || !y || which < 0 || which > 9) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
     if ((which == 4 || which == 5) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "phi bounds take pairs (n even)");
+    if ((which == 8 || which == 9) && (n & 3))
+        return set_error(QKD_ERR_INVALID_ARG, "paired phi bounds take quadruples (n % 4 == 0)");
     if (n == 0) return QKD_OK;
     hipLaunchKernelGGL(math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, which,
                        x, y, n);

@@ -162,9 +162,12 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
 // intervals must certify); its magnitude is bounded in the phi domain
 // (qkd_spec.h). A b2c interval that does not exclude 0 (or is too
 // close to 0, or a sum too large, to certify) raises the abort bit of the
-// round. Pipelined as split_check_phase.
+// round. Two forms: spec_check_phase_paired (below) for b2c intervals, and
+// this one for the iteration after the folded first one, whose slots hold
+// the psi bounds of exact b2c already (psi_of_exact, spec_bit_phase), so only
+// the output bound is evaluated per edge. Pipelined as split_check_phase.
 template <int DC>
-__device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
+__device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ plan, const uint32_t* tsyn,
                                                  const SplitStore<double>& ms, double* row, int n_tasks,
                                                  uint32_t n_pad, uint32_t n_bits, float thr_dn, float thr_up,
                                                  uint32_t* round_word, int wave, int lane) {
@@ -180,14 +183,14 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
     // n_pad < 2^24 and rows < 32: a 24-bit multiply
     auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
     auto edge = [&](double xv, uint2 w) -> double {
+        // phi(|b2c|) / ln 2 with the sign of b2c in the low word, NaN when
+        // the sign is not certain (psi_of_exact); idle lanes (the dummy
+        // column) do not count
         const f2 bv = qkds::unpack_iv(xv);
-        const bool neg = bv.y < 0.0f;
-        const f2 ab = neg ? -bv.yx : bv;                   // |b2c| in [a, b]
-        // certified sign, magnitude >= 1e-30 (NaN fails); idle lanes (the
-        // dummy column) do not count
-        const bool ok = (neg || bv.x > 0.0f) && ab.x > 1.0e-30f;
+        const bool neg = bv.x < 0.0f;
+        const bool ok = bv.x == bv.x;
         bad |= !ok && pw_bit(w) != n_bits;
-        const f2 ph = ok ? qkds::phi_bounds(ab.x, ab.y) : f2{0.0f, 0.0f};   // phi(|b2c|) / ln 2
+        const f2 ph = ok ? (neg ? -bv.yx : bv) : f2{0.0f, 0.0f};
         row[lane] = qkds::pack_iv(ph);
         const uint64_t sgn = __ballot(neg);
         wave_lds_sync();
@@ -247,6 +250,95 @@ __device__ __forceinline__ void spec_check_phase(const uint2* __restrict__ plan,
         wa = wc;
     }
     ms.st(pend, pv);
+    if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
+}
+
+// The same check phase with the input bound of the NEXT task's edge and the
+// output bound of this task's edge evaluated together (qkds::phi_pair: one
+// packed binary32 evaluation instead of two scalar ones). Per task t, in
+// order: the next task's b2c unpacked; this task's extrinsic sums from the
+// wave's row (written one iteration earlier); the pair; this task's c2b
+// stored; the next task's bounds into the row (after this task's row reads:
+// a wave's LDS accesses complete in order). Slots are loaded one task ahead
+// of their input bound, plan words two.
+template <int DC>
+__device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict__ plan, const uint32_t* tsyn,
+                                                        const SplitStore<double>& ms, double* row, int n_tasks,
+                                                        uint32_t n_pad, uint32_t n_bits, float thr_dn, float thr_up,
+                                                        uint32_t* round_word, int wave, int lane) {
+    using qkds::f2;
+    constexpr int NW = kDecodeBlock / 64;
+    int t = wave;
+    if (t >= n_tasks) return;
+    bool bad = false;
+    const uint2* pl = plan + lane;
+    if (lane < DC) row[64 + lane] = 0.0;
+    auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
+    // |b2c| of an edge, its sign and whether the interval certifies it
+    // (idle lanes, the dummy column, do not count)
+    auto input = [&](double xv, uint2 w, bool& neg, f2& ab) -> bool {
+        const f2 bv = qkds::unpack_iv(xv);
+        neg = bv.y < 0.0f;
+        ab = neg ? -bv.yx : bv;
+        const bool ok = (neg || bv.x > 0.0f) && ab.x > 1.0e-30f;
+        bad |= !ok && pw_bit(w) != n_bits;
+        return ok;
+    };
+    // (the plan has kPlanPadTasks idle tasks past n_tasks: loads ahead need no test)
+    uint2 wt = pl[t * 64];
+    uint2 wn = pl[(t + NW) * 64];
+    uint2 wnn = pl[(t + 2 * NW) * 64];
+    bool neg_t;
+    {
+        f2 ab;
+        const bool ok = input(ms.ld(slot(wt)), wt, neg_t, ab);
+        row[lane] = qkds::pack_iv(ok ? qkds::phi_bounds(ab.x, ab.y) : f2{0.0f, 0.0f});
+    }
+    uint64_t sgn_t = __ballot(neg_t);
+    double xn = ms.ld(slot(wn));
+    for (;;) {
+        const uint2 w3 = pl[(t + 3 * NW) * 64];
+        const double xnn = ms.ld(slot(wnn));
+        bool neg_n;
+        f2 ab_n;
+        const bool ok_n = input(xn, wn, neg_n, ab_n);
+        // this task's extrinsic sums (as spec_check_phase_psi)
+        wave_lds_sync();
+        const int start = pw_start(wt);
+        const int deg = pw_deg(wt);
+        f2 sum = f2{0.0f, 0.0f};
+        const uint32_t wmask = ((1u << deg) - 1u) & ~(1u << (uint32_t)(lane - start));
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const f2 o = qkds::unpack_iv(row[start + k]);
+            sum = __builtin_elementwise_fma(o, f2((float)((wmask >> k) & 1u)), sum);
+        }
+        const float nr = DC <= 8 ? (float)(DC + 2) : (float)(deg + 2);
+        const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
+        f2 ext = sum + f2{-mg, mg};
+        ext.x = ext.x > 0.0f ? ext.x : 0.0f;
+        bad |= !(ext.y < qkds::kPsiSumMax);
+        f2 ph_n, m;
+        qkds::phi_pair(ab_n.x, ab_n.y, ext.x, ext.y, ph_n, m);
+        // this task's c2b: threshold_matrix (:246-249) on the magnitude, the sign
+        m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
+        m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
+        const uint32_t j = pw_chk(wt);
+        const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
+        const uint32_t sigma =
+            sj ^ (uint32_t)(DC <= 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^ (neg_t ? 1u : 0u);
+        ms.st(slot(wt), qkds::pack_iv(sigma ? -m.yx : m));
+        // the next task's input bounds into the row
+        row[lane] = qkds::pack_iv(ok_n ? ph_n : f2{0.0f, 0.0f});
+        sgn_t = __ballot(neg_n);
+        neg_t = neg_n;
+        t += NW;
+        if (t >= n_tasks) break;
+        wt = wn;
+        wn = wnn;
+        wnn = w3;
+        xn = xnn;
+    }
     if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
 }
 
@@ -323,19 +415,22 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 for (int k = 0; k < kDvUnroll; ++k) acc = (DV3 || k < deg) ? acc + cv[k] : acc;
                 z = ok && acc <= 0;
 #pragma unroll
-                for (int k = 0; k < kDvUnroll; ++k) bo[k] = qkds::iv_of(clamp_msg(acc - cv[k], a.thr));
+                for (int k = 0; k < kDvUnroll; ++k) bo[k] = qkds::psi_of_exact(clamp_msg(acc - cv[k], a.thr));
             } else {
                 f2 L;
                 if constexpr (MODE == kModeLlr) L = qkds::iv_of(ok ? a.llr[(size_t)f * c.n + i] : 0.0);
                 else L = bob ? f2{-a.lp_up, -a.lp_dn} : f2{a.lp_dn, a.lp_up};
                 f2 cs[kDvUnroll];
                 f2 T = L;
-                float mag = __builtin_fmaxf(__builtin_fabsf(L.x), __builtin_fabsf(L.y));
+                // max(|lo|, |hi|) of an interval lo <= hi is max(hi, -lo) (med3
+                // with +inf: a max without canonicalising its operands)
+                auto amax = [](f2 x) { return __builtin_amdgcn_fmed3f(x.y, -x.x, __builtin_inff()); };
+                float mag = amax(L);
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) {
                     cs[k] = (DV3 || k < deg) ? qkds::unpack_iv(v[u][k]) : f2{0.0f, 0.0f};
                     T = T + cs[k];
-                    mag = mag + __builtin_fmaxf(__builtin_fabsf(cs[k].x), __builtin_fabsf(cs[k].y));
+                    mag = mag + amax(cs[k]);
                 }
                 // binary32 roundings (the sum here and the subtraction below)
                 // and the reference's binary64 ones, relative to the magnitudes
@@ -582,9 +677,15 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             uint32_t* rw = ctl + 4 + (rnd & 1u);
             if (SPEC && spec) {
                 if constexpr (SPEC) {
-                    if (!folded) {
-                        spec_check_phase<DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
-                                             a.thr_up, rw, wave, lane);
+                    // (iteration 2 after the folded first one: the slots hold
+                    // the phi bounds of exact b2c, psi_of_exact)
+                    if (!folded && fold1 && it == 1) {
+                        spec_check_phase_psi<DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
+                                                   a.thr_up, rw, wave, lane);
+                        __syncthreads();
+                    } else if (!folded) {
+                        spec_check_phase_paired<DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
+                                                    a.thr_up, rw, wave, lane);
                         __syncthreads();
                     }
                 }
@@ -764,6 +865,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                 } else if (!fold1) {    // the LLR path starts from LLR_i in every slot again
                     init_slots(false);
                     __syncthreads();
+                } else if (tid == 0) {
+                    // the dummy column's slot back to table index 0 (the
+                    // interval phases' idle lanes wrote it; read next by the
+                    // second check phase, after the folded bit phase's barrier)
+                    ms.st((uint32_t)c.n, (T)0);
                 }
                 if (tid == 0) {
                     atomicAdd(a.replay_count, 1u);
@@ -786,6 +892,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                 } else if (!fold1) {
                     init_slots(false);
                     __syncthreads();
+                } else if (tid == 0) {
+                    ms.st((uint32_t)c.n, (T)0);    // (as above)
                 }
                 if (tid == 0) {
                     atomicAdd(a.replay_count, 1u);

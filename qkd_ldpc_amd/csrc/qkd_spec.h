@@ -148,6 +148,62 @@ __device__ __forceinline__ void phi_bounds_out(float s_lo, float s_hi, float& lo
     hi = r.y;
 }
 
+// phi_bounds and phi_bounds_out evaluated together, one in each half of the
+// packed binary32 unit (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 issue at
+// almost the cost of one scalar instruction for both halves): the check
+// phase pairs the input bound of one task's edge (half 0, psi units) with the
+// output bound of the previous task's edge (half 1). Every operation is the
+// one the scalar forms above perform, so each half is bit for bit their
+// result (tests/test_spec.py compares them); only the transcendentals, the
+// selects and the argument split of half 0 stay scalar.
+__device__ __forceinline__ void phi_pair(float a, float b, float s_lo, float s_hi, f2& in, f2& out) {
+    // evaluation points: phi_bounds at a1 = min(a, kPhiHuge); phi_bounds_out
+    // at P = min(s_lo, kPsiHuge) (s_hi when the sum reached zero), x = P ln 2
+    const float a1 = __builtin_amdgcn_fmed3f(a, 0.0f, kPhiHuge);
+    const bool zero = !(s_lo > 0.0f);
+    const float P = __builtin_fminf(zero ? s_hi : s_lo, kPsiHuge);
+    // u = e^-x: half 0 by exp_neg's argument split, half 1 = 2^-P
+    const float L = 1.44269502162933349609375f;
+    const float L_lo = 1.925963033500011079e-08f;
+    const float p0 = a1 * L;
+    const float rl = __builtin_fmaf(__builtin_fmaf(a1, L, -p0), kLn2, a1 * (L_lo * kLn2));
+    const f2 e2 = f2{__builtin_amdgcn_exp2f(-p0), __builtin_amdgcn_exp2f(-P)};
+    const f2 u = f2{__builtin_fmaf(e2.x, -rl, e2.x), e2.y};
+    const f2 x = f2{a1, P * kLn2};
+    // phi_core, both halves (half 0 in psi units)
+    f2 t = __builtin_elementwise_fma(x, f2(1.0f / 5040.0f), f2(-1.0f / 720.0f));
+    t = __builtin_elementwise_fma(x, t, f2(1.0f / 120.0f));
+    t = __builtin_elementwise_fma(x, t, f2(-1.0f / 24.0f));
+    t = __builtin_elementwise_fma(x, t, f2(1.0f / 6.0f));
+    t = __builtin_elementwise_fma(x, t, f2(-0.5f));
+    t = __builtin_elementwise_fma(x, t, f2(1.0f));
+    const f2 ws = x * t;
+    const f2 wd = f2(1.0f) - u;
+    const f2 w = f2{x.x < 0.35f ? ws.x : wd.x, x.y < 0.35f ? ws.y : wd.y};
+    const f2 w2 = f2(2.0f) - w;
+    const f2 rw = f2{__builtin_amdgcn_rcpf(w.x), __builtin_amdgcn_rcpf(w.y)};
+    const f2 arg = w2 * rw;
+    const float lg1 = __builtin_amdgcn_logf(arg.y);
+    const f2 vlo = f2{__builtin_amdgcn_logf(arg.x), kLn2 * lg1};
+    const f2 s = u * u;
+    f2 h = __builtin_elementwise_fma(s, f2(1.0f / 13.0f), f2(1.0f / 11.0f));
+    h = __builtin_elementwise_fma(s, h, f2(1.0f / 9.0f));
+    h = __builtin_elementwise_fma(s, h, f2(1.0f / 7.0f));
+    h = __builtin_elementwise_fma(s, h, f2(0.2f));
+    h = __builtin_elementwise_fma(s, h, f2(1.0f / 3.0f));
+    h = __builtin_elementwise_fma(s, h, f2(1.0f));
+    const f2 vhi = (u * f2{2.0f * kInvLn2, 2.0f}) * h;
+    const f2 v = f2{x.x < 1.0f ? vlo.x : vhi.x, x.y < 1.0f ? vlo.y : vhi.y};
+    const f2 slope = (f2(2.0f) * u) * rw;
+    // the bounds: phi(a) widened up; the tangent at the evaluation point, down
+    const f2 hi = __builtin_elementwise_fma(v, f2(kPhiRel), v) + f2(1.0e-37f);
+    const f2 tn = __builtin_elementwise_fma(
+        -slope * f2{(1.0f + 2.0f * kPhiRel) * kInvLn2, (1.0f + 2.0f * kPhiRel) * kLn2}, f2{b, s_hi} - f2{a1, P},
+        v * f2(1.0f - kPhiRel));
+    in = f2{tn.x > 0.0f ? tn.x : 0.0f, hi.x};
+    out = f2{tn.y > 0.0f ? tn.y : 0.0f, zero ? __builtin_inff() : hi.y};
+}
+
 // An interval enclosing a finite binary64 value: its binary32 rounding
 // widened by 2^-22 relative (twice the rounding error and the widening's own)
 // and 1e-38 absolute (0 and subnormals give an interval containing 0).
@@ -155,6 +211,21 @@ __device__ __forceinline__ f2 iv_of(double x) {
     const float f = (float)x;
     const float a = __builtin_fabsf(f);
     return f2{__builtin_fmaf(a, -0x1.0p-22f, f) - 1.0e-38f, __builtin_fmaf(a, 0x1.0p-22f, f) + 1.0e-38f};
+}
+
+// The folded first bit phase's b2c are exact binary64 values: it stores, in
+// place of their intervals, the psi bounds the next check phase would compute
+// from those intervals (bit for bit the same), with the sign of b2c carried by
+// the low word: [lo, hi] for b2c > 0, [-hi, -lo] for b2c < 0 (hi > 0, so the
+// low word is negative exactly then); NaN for a b2c whose sign is not certain
+// (0 or NaN: the check phase aborts the round).
+__device__ __forceinline__ f2 psi_of_exact(double b) {
+    const f2 iv = iv_of(b);
+    const bool neg = iv.y < 0.0f;
+    const f2 ab = neg ? -iv.yx : iv;
+    const bool ok = (neg || iv.x > 0.0f) && ab.x > 1.0e-30f;
+    const f2 ph = phi_bounds(ab.x, ab.y);
+    return ok ? (neg ? -ph.yx : ph) : f2{__builtin_nanf(""), __builtin_nanf("")};
 }
 
 // An interval travels through the double-width message slots as its bits.

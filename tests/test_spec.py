@@ -112,6 +112,34 @@ def test_phi_bounds_contain_phi(Q, rel):
             assert err[k] < 0.5 * R
 
 
+def test_phi_pair_equals_scalar_forms(Q):
+    """The packed evaluation the check phase uses (qkds::phi_pair: the input
+    bound of one edge and the output bound of another in the two halves of the
+    packed binary32 unit) is bit for bit phi_bounds + phi_bounds_out, so the
+    certification of the scalar forms (the sweep above, the exhaustive sweep in
+    test_spec_bounds.py) carries over."""
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    a = np.exp(rng.uniform(np.log(1e-30), np.log(120.0), n)).astype(np.float32)
+    b = np.maximum(a, (a * (1.0 + rng.choice([0.0, 1e-6, 1e-3, 0.3], n))).astype(np.float32))
+    s_lo = np.exp(rng.uniform(np.log(1e-12), np.log(900.0), n)).astype(np.float32)
+    s_lo[rng.random(n) < 0.05] = 0.0                  # a widened sum that reached zero
+    s_hi = np.maximum(s_lo, (s_lo * (1.0 + rng.choice([0.0, 1e-6, 1e-3, 0.3], n)) + 1e-14).astype(np.float32))
+    # special points: the branch edges of phi_core and the clamps
+    a[:8] = [0.35, 1.0, 80.0, 120.0, 1e-30, 2.0, np.nextafter(np.float32(0.35), 0), np.nextafter(np.float32(1), 0)]
+    b[:8] = np.maximum(a[:8], b[:8])
+    x = np.stack([a, b, s_lo, s_hi], axis=1).astype(np.float64).ravel()
+    dx = torch.from_numpy(x).cuda()
+    out = {}
+    for which in (8, 9):
+        dy = torch.empty_like(dx)
+        Q._native.check(Q._native.lib().qkd_debug_math(which, dx.data_ptr(), dy.data_ptr(), dx.numel(), None))
+        torch.cuda.synchronize()
+        out[which] = dy.cpu().numpy().astype(np.float32).view(np.uint32)
+    bad = np.nonzero(out[8] != out[9])[0]
+    assert bad.size == 0, (bad[:8], x[bad[:8]], out[8][bad[:8]], out[9][bad[:8]])
+
+
 def test_phi_bounds_out_at_zero(Q):
     """A phi-domain sum that may be 0 (the reference's P / t can be exactly +-1)
     has an infinite upper bound."""
