@@ -1056,7 +1056,9 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
         size_t budget = kLdsBytesMax;
         if (const char* b = getenv("QKD_SPLIT_BUDGET")) budget = std::min(budget, (size_t)atol(b));
         const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, esz, budget);
-        if (L.bytes <= kLdsBytesMax && L.S > (uint32_t)c->n) {
+        // (the binary32 rule's kernel keeps every slot in LDS: SplitStore<float, true>)
+        const bool fits = rule == kRuleSp32 ? L.S >= (uint32_t)((size_t)c->max_dv * c->n_pad) : L.S > (uint32_t)c->n;
+        if (L.bytes <= kLdsBytesMax && fits) {
             int grid = 0;
             qkd_status s = decode_grid(c, sfn, L.bytes, &grid);
             if (s != QKD_OK) return s;

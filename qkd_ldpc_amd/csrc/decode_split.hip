@@ -65,7 +65,9 @@ template <> struct BufIo<float> {
     }
 };
 
-template <typename T>
+// ALL: every slot is in LDS (the host launches that instantiation only when
+// they fit): plain LDS accesses.
+template <typename T, bool ALL = false>
 struct SplitStore {
     T* l;                        // LDS slots [0, S) and the trash slots [S, S + 64)
     __amdgpu_buffer_rsrc_t g;    // global slots S.. of this workgroup
@@ -73,12 +75,17 @@ struct SplitStore {
     // (for x < S the buffer offset (x - S) * size wraps to at least
     // 2^32 - S * size, far past the region: out of range without a select)
     __device__ __forceinline__ T ld(uint32_t x) const {
+        if constexpr (ALL) return l[x];
         const bool in = x < S;
         const T vl = l[in ? x : 0u];
         const T vg = BufIo<T>::ld(g, (x - S) * (uint32_t)sizeof(T));
         return in ? vl : vg;
     }
     __device__ __forceinline__ void st(uint32_t x, T v) const {
+        if constexpr (ALL) {
+            l[x] = v;
+            return;
+        }
         const bool in = x < S;
         l[in ? x : S + (threadIdx.x & 63u)] = v;
         BufIo<T>::st(g, (x - S) * (uint32_t)sizeof(T), v);
@@ -87,11 +94,11 @@ struct SplitStore {
     // first slot, wave-uniform, a multiple of 64 as S is: SplitLds): all in
     // LDS or all global, one kind of access
     __device__ __forceinline__ T ld_row(uint32_t xw, uint32_t x) const {
-        if (xw < S) return l[x];
+        if (ALL || xw < S) return l[x];
         return BufIo<T>::ld(g, (x - S) * (uint32_t)sizeof(T));
     }
     __device__ __forceinline__ void st_row(uint32_t xw, uint32_t x, T v) const {
-        if (xw < S)
+        if (ALL || xw < S)
             l[x] = v;
         else
             BufIo<T>::st(g, (x - S) * (uint32_t)sizeof(T), v);
@@ -105,9 +112,9 @@ struct SplitStore {
 // task ahead are loaded before this task's arithmetic; stores trail by one
 // task. Slots of different tasks are distinct (idle lanes share the dummy
 // column's slot, whose value nothing reads).
-template <int SRC, bool CLAMP, int DC, int RULE, typename T>
+template <int SRC, bool CLAMP, int DC, int RULE, typename T, typename MS>
 __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
-                                                  const double* tab2, const SplitStore<T>& ms, T* row,
+                                                  const double* tab2, const MS& ms, T* row,
                                                   int n_tasks, uint32_t n_pad, T thr, int wave, int lane) {
     constexpr int NW = kDecodeBlock / 64;
     int t = wave;
@@ -153,6 +160,136 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
         wa = wc;
     }
     ms.st(pend, pv);
+}
+
+// ---- the binary32 variant (kRuleSp32, oracle/variants.py) -------------------
+// Check phase of the binary32 rule (edge_out's Gallager form, bit for bit):
+// psi(|b2c|) of the NEXT task's edge and phi of this task's extrinsic sum in
+// one packed evaluation (RuleMath<kRuleSp32>::pair), the message sign as the
+// segment parity of one ballot. The row holds the magnitudes |psi|; the sum
+// adds them in ascending lane order with weight 0 for this lane and for lanes
+// past the segment (x + 0 * y = x exactly), as edge_out skips them. Every slot
+// is in LDS (SplitStore<float, true>). Otherwise pipelined as
+// spec_check_phase_paired.
+template <bool CLAMP, int DC, typename MS>
+__device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
+                                                 const MS& ms, float* row, int n_tasks, uint32_t n_pad,
+                                                 float thr, int wave, int lane) {
+    constexpr int NW = kDecodeBlock / 64;
+    int t = wave;
+    if (t >= n_tasks) return;
+    const uint2* pl = plan + lane;
+    if (lane < DC) row[64 + lane] = 0.0f;
+    auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
+    uint2 wt = pl[t * 64];
+    uint2 wn = pl[(t + NW) * 64];
+    uint2 wnn = pl[(t + 2 * NW) * 64];
+    float xt = ms.ld(slot(wt));
+    row[lane] = __builtin_fabsf(RuleMath<kRuleSp32>::tanh_half(xt));
+    uint64_t sgn_t = __ballot(xt < 0.0f);
+    bool neg_t = xt < 0.0f;
+    float xn = ms.ld(slot(wn));
+    for (;;) {
+        const uint2 w3 = pl[(t + 3 * NW) * 64];
+        const float xnn = ms.ld(slot(wnn));
+        wave_lds_sync();
+        const int start = pw_start(wt);
+        const int deg = pw_deg(wt);
+        const uint32_t wmask = ((1u << deg) - 1u) & ~(1u << (uint32_t)(lane - start));
+        float S = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) S = __builtin_fmaf(row[start + k], (float)((wmask >> k) & 1u), S);
+        const qkds::f2 pv = RuleMath<kRuleSp32>::pair(xn, S);
+        const uint32_t j = pw_chk(wt);
+        const uint32_t neg = ((tsyn[j >> 5] >> (j & 31)) & 1u) ^
+                             (uint32_t)(DC <= 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^
+                             (neg_t ? 1u : 0u);
+        float v = neg ? -pv.y : pv.y;
+        if (CLAMP) v = clamp_msg(v, thr);
+        ms.st(slot(wt), v);
+        row[lane] = pv.x;
+        sgn_t = __ballot(xn < 0.0f);
+        neg_t = xn < 0.0f;
+        t += NW;
+        if (t >= n_tasks) break;
+        wt = wn;
+        wn = wnn;
+        wnn = w3;
+        xn = xnn;
+    }
+}
+
+// Bit phase of the binary32 rule over DeviceCode::bit_code (one load per bit
+// for its checks and their degrees): total = LLR + c2b_0 + c2b_1 + ...
+// ascending (:256-267), the hard decision and its syndrome, b2c_k =
+// clamp(total - c2b_k) (:303-316); FOLD: the first iteration's messages
+// +-C_d (fold_first_message). The operations of the generic bit phase.
+constexpr int kSp32Chunk = 3;     // bit-phase rounds per load batch
+template <bool FOLD, int MODE, bool CLAMP, typename MS>
+__device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const DecodeArgs& a, const MS& ms,
+                                               const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
+                                               uint64_t* zw, uint32_t bobmask, bool keep, uint32_t f, int tid,
+                                               int wave, int lane) {
+    const uint32_t n_pad = (uint32_t)c.n_pad;
+    const float llr_p = (float)a.log_p;
+    const float thr = (float)a.thr;
+    const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
+    for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kSp32Chunk) {
+        float v[kSp32Chunk][kDvUnroll];
+        uint64_t bc[kSp32Chunk];
+#pragma unroll
+        for (int u = 0; u < kSp32Chunk; ++u) {
+            const int i = tid + (r0 + u) * kDecodeBlock;
+            const bool ok = i < c.n;
+            bc[u] = ok ? c.bit_code[i] : 0;
+#pragma unroll
+            for (int k = 0; k < kDvUnroll; ++k) v[u][k] = (FOLD || !ok) ? 0.0f : ms.ld((uint32_t)k * n_pad + i);
+        }
+#pragma unroll
+        for (int u = 0; u < kSp32Chunk; ++u) {
+            const int r = r0 + u;
+            if (r * kDecodeBlock >= c.n) break;            // block-uniform
+            const int i = tid + r * kDecodeBlock;
+            const bool ok = i < c.n;
+            const int deg = (int)(bc[u] >> 48) & 3;
+            int32_t jc[kDvUnroll];
+#pragma unroll
+            for (int k = 0; k < kDvUnroll; ++k) jc[k] = (int32_t)(bc[u] >> (16 * k)) & 0xffff;
+            const uint32_t bob = (bobmask >> r) & 1u;
+            float acc;
+            if constexpr (MODE == kModeLlr) acc = ok ? (float)a.llr[(size_t)f * c.n + i] : 0.0f;
+            else acc = bob ? -llr_p : llr_p;
+            if (FOLD) {
+                const uint32_t sgi = bob ^ lsign;
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k) {
+                    const int j = jc[k];
+                    const uint32_t sp = (qsyn[j >> 5] >> (j & 31)) & 1u;
+                    const float cm = (float)ctab[((uint32_t)(bc[u] >> (50 + 4 * k)) & 15u) + 1u];
+                    v[u][k] = (sp ^ sgi) ? -cm : cm;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
+            const bool z = ok && acc <= 0.0f;
+            const uint64_t zb = __ballot(z);
+            if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
+            if (z) {
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k)
+                    if (k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
+            }
+            if (!keep || !ok) continue;
+#pragma unroll
+            for (int k = 0; k < kDvUnroll; ++k) {
+                if (k < deg) {
+                    float b = acc - v[u][k];
+                    if (CLAMP) b = clamp_msg(b, thr);
+                    ms.st((uint32_t)k * n_pad + i, b);
+                }
+            }
+        }
+    }
 }
 
 // ---- speculative interval iterations (qkd_spec.h) ---------------------------
@@ -513,7 +650,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
     double* tab2 = reinterpret_cast<double*>(smem + L.tab2);
-    const SplitStore<T> ms{
+    using MS = SplitStore<T, RULE == kRuleSp32>;
+    const MS ms{
         reinterpret_cast<T*>(smem + L.msg),
         __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<T*>(a.c2b) + (size_t)blockIdx.x * a.c2b_stride, (short)0,
                                           (int)(a.c2b_stride * sizeof(T)), 0x00020000),
@@ -690,7 +828,9 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     }
                 }
             } else if (!folded) {
-                if (TABLES && it == 1 && tab2_on)
+                if constexpr (RULE == kRuleSp32)
+                    sp32_check_phase<CLAMP, DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, thr, wave, lane);
+                else if (TABLES && it == 1 && tab2_on)
                     split_check_phase<kSrcTable, CLAMP, DC, RULE>(c.plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);
                 else
@@ -721,6 +861,15 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                             spec_bit_phase<false, MODE, false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
                                                                f, tid, wave, lane);
                     }
+                }
+            } else if (RULE == kRuleSp32 && c.bit_code != nullptr) {
+                if constexpr (RULE == kRuleSp32) {
+                    if (folded)
+                        sp32_bit_phase<true, MODE, CLAMP>(c, a, ms, qsyn, ctab, xsyn, zw, bobmask, keep, f, tid, wave,
+                                                          lane);
+                    else
+                        sp32_bit_phase<false, MODE, CLAMP>(c, a, ms, qsyn, ctab, xsyn, zw, bobmask, keep, f, tid,
+                                                           wave, lane);
                 }
             } else
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += BC) {

@@ -276,6 +276,22 @@ template <> struct RuleMath<kRuleSp32> {
         const float at = s > qkds::kPsiHuge ? qkds::kPsiHuge : s;
         return qkds::phi_core<false>(at * qkds::kLn2, __builtin_amdgcn_exp2f(-at)).v;
     }
+    // |tanh_half(x)| (half 0) and two_atanh(s) (half 1) in one packed
+    // evaluation (qkds::phi_core_pair): bit for bit the two functions above
+    static __device__ __forceinline__ qkds::f2 pair(float x, float s) {
+        float a = __builtin_fabsf(x);
+        a = a < 1.0e-30f ? 1.0e-30f : a;
+        a = a > qkds::kPhiHuge ? qkds::kPhiHuge : a;
+        const float at = s > qkds::kPsiHuge ? qkds::kPsiHuge : s;
+        // exp_neg(a) (argument split) and 2^-at
+        const float L = 1.44269502162933349609375f;
+        const float L_lo = 1.925963033500011079e-08f;
+        const float p = a * L;
+        const float rl = __builtin_fmaf(__builtin_fmaf(a, L, -p), qkds::kLn2, a * (L_lo * qkds::kLn2));
+        const float e0 = __builtin_amdgcn_exp2f(-p);
+        const qkds::f2 u = qkds::f2{__builtin_fmaf(e0, -rl, e0), __builtin_amdgcn_exp2f(-at)};
+        return qkds::phi_core_pair(qkds::f2{a, at * qkds::kLn2}, u).v;
+    }
 };
 
 // A check-phase message store. (Non-temporal stores, which skip L2, measured

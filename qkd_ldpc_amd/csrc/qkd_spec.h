@@ -148,29 +148,14 @@ __device__ __forceinline__ void phi_bounds_out(float s_lo, float s_hi, float& lo
     hi = r.y;
 }
 
-// phi_bounds and phi_bounds_out evaluated together, one in each half of the
-// packed binary32 unit (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 issue at
-// almost the cost of one scalar instruction for both halves): the check
-// phase pairs the input bound of one task's edge (half 0, psi units) with the
-// output bound of the previous task's edge (half 1). Every operation is the
-// one the scalar forms above perform, so each half is bit for bit their
-// result (tests/test_spec.py compares them); only the transcendentals, the
-// selects and the argument split of half 0 stay scalar.
-__device__ __forceinline__ void phi_pair(float a, float b, float s_lo, float s_hi, f2& in, f2& out) {
-    // evaluation points: phi_bounds at a1 = min(a, kPhiHuge); phi_bounds_out
-    // at P = min(s_lo, kPsiHuge) (s_hi when the sum reached zero), x = P ln 2
-    const float a1 = __builtin_amdgcn_fmed3f(a, 0.0f, kPhiHuge);
-    const bool zero = !(s_lo > 0.0f);
-    const float P = __builtin_fminf(zero ? s_hi : s_lo, kPsiHuge);
-    // u = e^-x: half 0 by exp_neg's argument split, half 1 = 2^-P
-    const float L = 1.44269502162933349609375f;
-    const float L_lo = 1.925963033500011079e-08f;
-    const float p0 = a1 * L;
-    const float rl = __builtin_fmaf(__builtin_fmaf(a1, L, -p0), kLn2, a1 * (L_lo * kLn2));
-    const f2 e2 = f2{__builtin_amdgcn_exp2f(-p0), __builtin_amdgcn_exp2f(-P)};
-    const f2 u = f2{__builtin_fmaf(e2.x, -rl, e2.x), e2.y};
-    const f2 x = f2{a1, P * kLn2};
-    // phi_core, both halves (half 0 in psi units)
+// phi_core twice, in the two halves of the packed binary32 unit: half 0 in
+// psi units (phi_core<true>), half 1 in phi units (phi_core<false>); every
+// operation is phi_core's, so each half is bit for bit its result.
+struct PhiVal2 {
+    f2 v;
+    f2 slope;
+};
+__device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u) {
     f2 t = __builtin_elementwise_fma(x, f2(1.0f / 5040.0f), f2(-1.0f / 720.0f));
     t = __builtin_elementwise_fma(x, t, f2(1.0f / 120.0f));
     t = __builtin_elementwise_fma(x, t, f2(-1.0f / 24.0f));
@@ -193,8 +178,35 @@ __device__ __forceinline__ void phi_pair(float a, float b, float s_lo, float s_h
     h = __builtin_elementwise_fma(s, h, f2(1.0f / 3.0f));
     h = __builtin_elementwise_fma(s, h, f2(1.0f));
     const f2 vhi = (u * f2{2.0f * kInvLn2, 2.0f}) * h;
-    const f2 v = f2{x.x < 1.0f ? vlo.x : vhi.x, x.y < 1.0f ? vlo.y : vhi.y};
-    const f2 slope = (f2(2.0f) * u) * rw;
+    PhiVal2 o;
+    o.v = f2{x.x < 1.0f ? vlo.x : vhi.x, x.y < 1.0f ? vlo.y : vhi.y};
+    o.slope = (f2(2.0f) * u) * rw;
+    return o;
+}
+
+// phi_bounds and phi_bounds_out evaluated together, one in each half of the
+// packed binary32 unit (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 issue at
+// almost the cost of one scalar instruction for both halves): the check
+// phase pairs the input bound of one task's edge (half 0, psi units) with the
+// output bound of the previous task's edge (half 1). Every operation is the
+// one the scalar forms above perform, so each half is bit for bit their
+// result (tests/test_spec.py compares them); only the transcendentals, the
+// selects and the argument split of half 0 stay scalar.
+__device__ __forceinline__ void phi_pair(float a, float b, float s_lo, float s_hi, f2& in, f2& out) {
+    // evaluation points: phi_bounds at a1 = min(a, kPhiHuge); phi_bounds_out
+    // at P = min(s_lo, kPsiHuge) (s_hi when the sum reached zero), x = P ln 2
+    const float a1 = __builtin_amdgcn_fmed3f(a, 0.0f, kPhiHuge);
+    const bool zero = !(s_lo > 0.0f);
+    const float P = __builtin_fminf(zero ? s_hi : s_lo, kPsiHuge);
+    // u = e^-x: half 0 by exp_neg's argument split, half 1 = 2^-P
+    const float L = 1.44269502162933349609375f;
+    const float L_lo = 1.925963033500011079e-08f;
+    const float p0 = a1 * L;
+    const float rl = __builtin_fmaf(__builtin_fmaf(a1, L, -p0), kLn2, a1 * (L_lo * kLn2));
+    const f2 e2 = f2{__builtin_amdgcn_exp2f(-p0), __builtin_amdgcn_exp2f(-P)};
+    const f2 u = f2{__builtin_fmaf(e2.x, -rl, e2.x), e2.y};
+    const PhiVal2 e = phi_core_pair(f2{a1, P * kLn2}, u);
+    const f2 v = e.v, slope = e.slope;
     // the bounds: phi(a) widened up; the tangent at the evaluation point, down
     const f2 hi = __builtin_elementwise_fma(v, f2(kPhiRel), v) + f2(1.0e-37f);
     const f2 tn = __builtin_elementwise_fma(
