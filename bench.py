@@ -39,6 +39,13 @@ B_FRAME = 2 * N_BITS + M_CHECKS                 # 25,711
 HBM_PEAK_GBS = 8000.0                           # MI355X_MICROARCH.md, HBM3E spec
 
 
+# decoder rules measured (include/qkd_ldpc.h QKD_VARIANT_*): the reference's,
+# and the build-defined binary32 variants; minsum_sc = self-corrected min-sum at
+# its best scale (profiles/r02_minsum_sweep.jsonl)
+VARIANTS = {"sp_f64": {"variant": "sp_f64"}, "sp_f32": {"variant": "sp_f32"}, "minsum": {"variant": "minsum"},
+            "minsum_sc": {"variant": "minsum", "minsum_scale": 0.875, "minsum_self_correct": True}}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -55,7 +62,7 @@ def parse():
                     help="CPU-baseline threads (capped at the CPUs this process may use)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (keygen + decode) line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--variant", default="sp_f64", choices=["sp_f64", "sp_f32", "minsum"],
+    ap.add_argument("--variant", default="sp_f64", choices=sorted(VARIANTS),
                     help="decoder rule of the headline line (sp_f64 = the reference's)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the side measurement of the binary32 variants")
@@ -107,12 +114,13 @@ def roofline_block(variant, alg_bytes, kernel_s, kernel_name):
 
 def measure_variants(args, step, stream, counters, iters, Q, F, q, steps=5):
     """Side measurement on the same resident keys: the build-defined binary32
-    variants (QKD_VARIANT_SP_F32, QKD_VARIANT_MINSUM),
+    variants (QKD_VARIANT_SP_F32, QKD_VARIANT_MINSUM plain and self-corrected;
+    SURVEY.md §8(d) config 5),
     timed like the headline (wall clock over `steps` steps, HIP events for the
     decode kernel). Their FER is a property of the decoder, not a parity claim."""
     import torch
     out = {}
-    for v in ("sp_f64", "sp_f32", "minsum"):
+    for v in VARIANTS:
         if v == args.variant:
             continue
         step(variant=v)
@@ -233,7 +241,7 @@ def main():
     sptr = int(stream.cuda_stream)
 
     def step(ev=None, variant=args.variant):
-        flags = Q.decoder_flags(True, variant)
+        flags = Q.decoder_flags(True, **VARIANTS[variant])
         if ev is not None:
             ev[0].record(stream)
         Q._native.check(L.qkd_qkd_ldpc_batch(H.handle, ws.handle, alice.data_ptr(), bob.data_ptr(), F,

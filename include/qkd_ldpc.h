@@ -85,6 +85,10 @@ typedef enum qkd_status {
  * is max(scale * min |b2c| - offset, 0) (offset min-sum); 0 = no offset. */
 #define QKD_MINSUM_OFFSET_SHIFT 16
 #define QKD_MINSUM_OFFSET(x) ((((uint32_t)((x) * 64.0 + 0.5)) & 0xffu) << QKD_MINSUM_OFFSET_SHIFT)
+/* Self-corrected min-sum (QKD_VARIANT_MINSUM only; needs the LDS-state
+ * min-sum kernel): a bit-to-check message whose sign flipped since the last
+ * iteration (both nonzero) is erased to 0 before the check rule. */
+#define QKD_MINSUM_SELF_CORRECT 0x1000000u
 
 typedef struct qkd_code qkd_code;
 typedef struct qkd_workspace qkd_workspace;

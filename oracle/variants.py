@@ -11,6 +11,9 @@ operation rounds exactly as the kernel's does:
   c2b           (-1)^(s_j + #negative other b2c) * max(scale * min over the other
                 |b2c| - offset, 0) (offset 0: plain normalised min-sum; NaN inputs
                 ignored by the min, as fminf), then clamp (:246-249)
+  self-correct  (QKD_MINSUM_SELF_CORRECT, Savin's self-corrected min-sum) from the
+                second iteration on, a b2c whose sign differs from the edge's
+                previous b2c, both nonzero, is erased to 0 before the check rule
   total         float(LLR_i) + c2b_0 + c2b_1 + ... in ascending check order (:256-267)
   stop          H z == s, z_i = total_i <= 0 (:277-285)
 """
@@ -56,7 +59,8 @@ class MinSumModel:
     def _clamp(v, thr):
         return np.where(v > thr, thr, np.where(v < -thr, -thr, v)).astype(np.float32)
 
-    def decode(self, llr, syndrome, max_it=50, thr=100.0, thr_enable=True, scale=0.8125, offset=0.0):
+    def decode(self, llr, syndrome, max_it=50, thr=100.0, thr_enable=True, scale=0.8125, offset=0.0,
+               self_correct=False):
         """llr [F, N] float64, syndrome [F, M] -> (bits [F, N] u8, iterations [F], sp_ok [F])."""
         llr32 = np.asarray(llr, np.float64).astype(np.float32)
         syn = np.asarray(syndrome, np.uint8)
@@ -71,12 +75,18 @@ class MinSumModel:
         live = np.ones(F, bool)
         valid = self.cslot >= 0
         cs = np.maximum(self.cslot, 0)
+        prev = None
         for it in range(max_it):
             b2c = total[:, self.bit_of_edge]
             if it > 0:
                 b2c = (b2c - c2b).astype(np.float32)
                 if thr_enable:
                     b2c = self._clamp(b2c, thr32)
+                if self_correct:
+                    with np.errstate(invalid="ignore"):
+                        er = (prev != 0) & (b2c != 0) & ((b2c < 0) != (prev < 0))
+                    b2c = np.where(er, np.float32(0), b2c).astype(np.float32)
+            prev = b2c
             B = b2c[:, cs]                                           # [F, M, DC]
             mag = np.where(valid[None], np.abs(B), np.float32(np.inf)).astype(np.float32)
             negb = ((B < 0) & valid[None]).astype(np.uint8)

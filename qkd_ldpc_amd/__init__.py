@@ -45,7 +45,8 @@ __all__ = [
 
 
 def decoder_flags(threshold_enabled: bool = True, variant: str = "sp_f64",
-                  minsum_scale: float | None = None, minsum_offset: float | None = None) -> int:
+                  minsum_scale: float | None = None, minsum_offset: float | None = None,
+                  minsum_self_correct: bool = False) -> int:
     """Flag word of the decode entry points: the reference's threshold switch
     (CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD) and the check-node rule:
     "sp_f64" (the reference, bit-exact), "sp_f32" or "minsum" (build-defined
@@ -67,6 +68,10 @@ def decoder_flags(threshold_enabled: bool = True, variant: str = "sp_f64",
         if not (0 <= q <= 255) or q != minsum_offset * 64:
             raise ValueError("minsum_offset must be k/64 for k in 0..255")
         flags |= q << N.MINSUM_OFFSET_SHIFT
+    if minsum_self_correct:
+        if variant != "minsum":
+            raise ValueError("minsum_self_correct applies to variant='minsum' only")
+        flags |= N.MINSUM_SELF_CORRECT
     return flags
 
 
@@ -264,7 +269,7 @@ def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
                          msg_threshold: float = 100.0, threshold_enabled: bool = True,
                          want_bits: bool = True, workspace=None, stream=None,
                          variant: str = "sp_f64", minsum_scale: float | None = None,
-                         minsum_offset: float | None = None) -> SPResult:
+                         minsum_offset: float | None = None, minsum_self_correct: bool = False) -> SPResult:
     """sum_product_decoding_irregular/_regular (qkd_ldpc_algorithm.cpp:3-345), batched.
     llr [F, N] float64, syndrome [F, M] uint8 (0/1)."""
     _need_cuda(llr, torch.float64, "llr", H)
@@ -275,7 +280,7 @@ def sum_product_decoding(H: HMatrix, llr, syndrome, max_iterations: int = 50,
     bits = torch.empty((f, H.num_bit_nodes), dtype=torch.uint8, device=dev) if want_bits else None
     iters = torch.empty(f, dtype=torch.int32, device=dev)
     ok = torch.empty(f, dtype=torch.uint8, device=dev)
-    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset)
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset, minsum_self_correct)
     N.check(N.lib().qkd_decode_batch(H.handle, _ws(workspace), _ptr(llr), _ptr(syndrome), f,
                                      max_iterations, msg_threshold, flags, _ptr(bits), _ptr(iters),
                                      _ptr(ok), _stream(stream, H.device)))
@@ -291,7 +296,7 @@ def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
              msg_threshold: float = 100.0, threshold_enabled: bool = True,
              want_bits: bool = False, workspace=None, stream=None,
              variant: str = "sp_f64", minsum_scale: float | None = None,
-             minsum_offset: float | None = None) -> LDPCResult:
+             minsum_offset: float | None = None, minsum_self_correct: bool = False) -> LDPCResult:
     """QKD_LDPC_irregular/_regular (qkd_ldpc_algorithm.cpp:347-447), batched.
     alice, bob [F, N] uint8 (0/1); one QBER for the batch."""
     _need_cuda(alice, torch.uint8, "alice", H)
@@ -303,7 +308,7 @@ def qkd_ldpc(H: HMatrix, alice, bob, qber: float, max_iterations: int = 50,
     iters = torch.empty(f, dtype=torch.int32, device=dev)
     ok = torch.empty(f, dtype=torch.uint8, device=dev)
     km = torch.empty(f, dtype=torch.uint8, device=dev)
-    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset)
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset, minsum_self_correct)
     N.check(N.lib().qkd_qkd_ldpc_batch(H.handle, _ws(workspace), _ptr(alice), _ptr(bob), f, qber,
                                        max_iterations, msg_threshold, flags, _ptr(bits),
                                        _ptr(iters), _ptr(ok), _ptr(km), _stream(stream, H.device)))
@@ -344,7 +349,8 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                max_iterations: int = 50, msg_threshold: float = 100.0,
                threshold_enabled: bool = True, workspace=None, stream=None,
                out: TrialResults | None = None, variant: str = "sp_f64",
-               minsum_scale: float | None = None, minsum_offset: float | None = None) -> TrialResults:
+               minsum_scale: float | None = None, minsum_offset: float | None = None,
+               minsum_self_correct: bool = False) -> TrialResults:
     """run_trial (simulation.cpp:161-189) for every frame, fused on the device, plus the
     per-QBER-point counters of simulation.cpp:252-312. seeds: int64 CUDA tensor holding
     the uint64 seed bits."""
@@ -365,7 +371,7 @@ def run_trials(H: HMatrix, seeds, q_nominal: float, seed_offset: int = 0,
                            torch.empty(f, dtype=torch.uint8, device=dev),
                            torch.empty(f, dtype=torch.float64, device=dev),
                            torch.empty(N.COUNTERS_BYTES, dtype=torch.uint8, device=dev))
-    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset)
+    flags = decoder_flags(threshold_enabled, variant, minsum_scale, minsum_offset, minsum_self_correct)
     N.check(N.lib().qkd_trials_batch(H.handle, _ws(workspace), _ptr(seeds), seed_offset, f,
                                      q_nominal, max_iterations, msg_threshold, flags,
                                      _ptr(out.iterations), _ptr(out.syndromes_match),

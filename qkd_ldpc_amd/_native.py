@@ -40,6 +40,7 @@ READ_SORT_ROWS = 0x1   # qkd_code_from_alist_ex
 VARIANTS = {"sp_f64": 0x00, "sp_f32": 0x10, "minsum": 0x20}
 MINSUM_SCALE_SHIFT = 8
 MINSUM_OFFSET_SHIFT = 16
+MINSUM_SELF_CORRECT = 1 << 24   # QKD_MINSUM_SELF_CORRECT
 MINSUM_DEFAULT_SCALE = 0.8125
 
 # Every symbol include/qkd_ldpc.h declares (checked by tests/test_abi.py).

@@ -124,6 +124,10 @@ __device__ __forceinline__ void check_phase(const uint2* __restrict__ plan, cons
 //   y  min2 = min over k != idx1 of |b2c_k|
 //   z  sign bits, bit k = (b2c_k < 0)
 //   w  idx1 (bits 0..7; 0xff: none) | par << 31,   par = s_j ^ parity(z)
+// and, self-corrected (QKD_MINSUM_SELF_CORRECT), a fifth word czf[j]: bit k =
+// (b2c_k == 0). z and czf are then also the previous iteration's b2c signs
+// and erasures, which the next check phase compares with (Savin's
+// self-corrected min-sum: a b2c whose sign flipped, both nonzero, becomes 0).
 // The message to the edge at position k is scale * (k == idx1 ? min2 : min1),
 // negated when par ^ z_k, then clamped: the same binary32 operations, on the
 // same values, as edge_out's min-sum branch (and tests/test_variants.py's model), so the
@@ -157,7 +161,8 @@ __device__ __forceinline__ float ms_msg(uint4 st, uint32_t pos, float scale, flo
 //   state = (min |b2c|, second min, argmin, signs, s_j ^ parity)
 template <int SRC, bool CLAMP, int DC>
 __device__ __forceinline__ void ms_check_phase(const DeviceCode& c, const uint32_t* tsyn, const float* total,
-                                               uint4* cst, float thr, float scale, float off) {
+                                               uint4* cst, uint32_t* czf, bool sc, float thr, float scale,
+                                               float off) {
     const int m = c.m;
     int j = threadIdx.x;
     if (j >= m) return;
@@ -174,9 +179,13 @@ __device__ __forceinline__ void ms_check_phase(const DeviceCode& c, const uint32
             for (int k = 0; k < DC; ++k) nb[k] = k < c.max_dc ? c.chk_bits[k * c.m_pad + jn] : -1;
         }
         uint4 st = make_uint4(0, 0, 0, 0);
-        if (SRC == kSrcGeneral) st = cst[j];
+        uint32_t zp = 0;
+        if (SRC == kSrcGeneral) {
+            st = cst[j];
+            if (sc) zp = czf[j];
+        }
         float m1 = __builtin_inff(), m2 = __builtin_inff();
-        uint32_t idx = 0xffu, sg = 0;
+        uint32_t idx = 0xffu, sg = 0, zf = 0;
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             if (bl[k] >= 0) {
@@ -184,9 +193,13 @@ __device__ __forceinline__ void ms_check_phase(const DeviceCode& c, const uint32
                 if (SRC == kSrcGeneral) {
                     x = x - ms_msg<CLAMP>(st, (uint32_t)k, scale, off, thr);
                     if (CLAMP) x = clamp_msg(x, thr);
+                    // self-correction: the previous b2c nonzero, this one too,
+                    // signs differ -> erased
+                    if (sc && !((zp >> k) & 1u) && x != 0.0f && (x < 0.0f) != (((st.z >> k) & 1u) != 0u)) x = 0.0f;
                 }
                 const float a = fabsf(x);
                 sg |= (x < 0.0f ? 1u : 0u) << k;
+                zf |= (x == 0.0f ? 1u : 0u) << k;
                 if (a < m1) {
                     m2 = m1;
                     m1 = a;
@@ -199,6 +212,7 @@ __device__ __forceinline__ void ms_check_phase(const DeviceCode& c, const uint32
         const uint32_t sbit = (tsyn[j >> 5] >> (j & 31)) & 1u;
         const uint32_t par = sbit ^ ((uint32_t)__popc(sg) & 1u);
         cst[j] = make_uint4(__float_as_uint(m1), __float_as_uint(m2), sg, idx | (par << 31));
+        if (sc) czf[j] = zf;
         j = jn;
         if (j >= m) break;
     }
@@ -282,8 +296,9 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
     const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries, GT ? 0 : (int)sizeof(T),
-                      MSL ? c.m : 0, (int)sizeof(T));
+                      MSL ? c.m : 0, (int)sizeof(T), MSL && a.ms_sc);
     uint4* cst = reinterpret_cast<uint4*>(smem + L.cst);
+    uint32_t* czf = reinterpret_cast<uint32_t*>(smem + L.czf);
     const int m_words = decode_m_words(c.m);
     T* total;
     if constexpr (GT)
@@ -423,9 +438,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             if constexpr (MSL) {
                 tabled = true;
                 if (it == 0)
-                    ms_check_phase<kSrcFirst, CLAMP, DC>(c, tsyn, total, cst, thr, a.ms_scale, a.ms_offset);
+                    ms_check_phase<kSrcFirst, CLAMP, DC>(c, tsyn, total, cst, czf, a.ms_sc != 0, thr, a.ms_scale,
+                                                         a.ms_offset);
                 else
-                    ms_check_phase<kSrcGeneral, CLAMP, DC>(c, tsyn, total, cst, thr, a.ms_scale, a.ms_offset);
+                    ms_check_phase<kSrcGeneral, CLAMP, DC>(c, tsyn, total, cst, czf, a.ms_sc != 0, thr, a.ms_scale,
+                                                           a.ms_offset);
             }
             if constexpr (TABLES) {
                 tabled = true;
@@ -902,10 +919,11 @@ static float minsum_scale_of(uint32_t flags) {
     return q ? (float)q / 256.0f : (float)QKD_MINSUM_DEFAULT_SCALE;
 }
 
-static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries, int rule, bool gt = false) {
+static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries, int rule, bool gt = false,
+                               bool sc = false) {
     const int esz = rule == kRuleSp64 ? 8 : 4;
     return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries, gt ? 0 : esz,
-                     rule == kRuleMinSumLds ? c->m : 0, esz).bytes;
+                     rule == kRuleMinSumLds ? c->m : 0, esz, rule == kRuleMinSumLds && sc).bytes;
 }
 
 static constexpr size_t kLdsBytesMax = 160 * 1024;
@@ -921,10 +939,10 @@ static bool decode_needs_gt(const qkd_code* c, int rule, int tab2_entries) {
 
 // The LDS-resident min-sum needs the check state (sign bits in one word:
 // degree <= 32) and all of its LDS in one workgroup.
-static bool decode_ms_fits(const qkd_code* c) {
+static bool decode_ms_fits(const qkd_code* c, bool sc) {
     if (c->max_dc > 32 || c->n > kMaxBitsLds) return false;
     const int dc = c->max_dc <= 4 ? 4 : c->max_dc <= 6 ? 6 : c->max_dc <= 8 ? 8 : c->max_dc <= 16 ? 16 : 32;
-    return decode_lds_bytes(c, dc, 0, kRuleMinSumLds) <= kLdsBytesMax;
+    return decode_lds_bytes(c, dc, 0, kRuleMinSumLds, false, sc) <= kLdsBytesMax;
 }
 
 // Resident workgroups of decode_kernel for this code on its device.
@@ -1039,7 +1057,11 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     // QKD_MINSUM_STORE=global keeps the global-message-store min-sum (tests)
     const char* ms_store = getenv("QKD_MINSUM_STORE");
     const bool ms_global = ms_store && !strcmp(ms_store, "global");
-    if (rule == kRuleMinSum && !ms_global && decode_ms_fits(c)) rule = kRuleMinSumLds;
+    a.ms_sc = (flags & QKD_MINSUM_SELF_CORRECT) ? 1 : 0;
+    if (rule == kRuleMinSum && !ms_global && decode_ms_fits(c, a.ms_sc != 0)) rule = kRuleMinSumLds;
+    if (a.ms_sc && rule != kRuleMinSumLds)
+        return set_error(QKD_ERR_UNSUPPORTED, "self-corrected min-sum needs the LDS-state min-sum kernel "
+                                              "(check degree <= 32, its state in LDS)");
     a.ms_scale = minsum_scale_of(flags);
     a.ms_offset = (float)((flags >> QKD_MINSUM_OFFSET_SHIFT) & 0xffu) / 64.0f;
     // The split-store kernel (decode_split.hip) for the sum-product rules
@@ -1128,7 +1150,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
         a.tab2_entries = 0;
     }
     DecodeFn fn = pick_decode(mode, rule, a.clamp_on != 0, c->max_dc, gt, &dc);
-    const size_t lds = decode_lds_bytes(c, dc, a.tab2_entries, rule, gt);
+    const size_t lds = decode_lds_bytes(c, dc, a.tab2_entries, rule, gt, a.ms_sc != 0);
     int grid = 0;
     qkd_status s = decode_grid(c, fn, lds, &grid);
     if (s != QKD_OK) return s;
@@ -1165,7 +1187,7 @@ static qkd_status check_frames(size_t n_frames) {
 static qkd_status check_decode_params(uint32_t max_it, double thr, uint32_t flags) {
     if (max_it < 1) return set_error(QKD_ERR_INVALID_ARG, "max_iterations must be >= 1");
     const uint32_t known = QKD_FLAG_THRESHOLD | QKD_VARIANT_MASK | (0xffu << QKD_MINSUM_SCALE_SHIFT) |
-                           (0xffu << QKD_MINSUM_OFFSET_SHIFT);
+                           (0xffu << QKD_MINSUM_OFFSET_SHIFT) | QKD_MINSUM_SELF_CORRECT;
     if (flags & ~known) return set_error(QKD_ERR_INVALID_ARG, "unknown flags 0x%x", flags);
     if ((flags & QKD_VARIANT_MASK) == QKD_VARIANT_MASK)
         return set_error(QKD_ERR_INVALID_ARG, "unknown decoder variant 0x%x", flags & QKD_VARIANT_MASK);

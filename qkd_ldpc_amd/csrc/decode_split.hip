@@ -162,7 +162,7 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
     ms.st(pend, pv);
 }
 
-// ---- the binary32 variant (kRuleSp32, oracle/variants.py) -------------------
+// ---- the binary32 variant (kRuleSp32; specification: tests/test_variants.py) 
 // Check phase of the binary32 rule (edge_out's Gallager form, bit for bit):
 // psi(|b2c|) of the NEXT task's edge and phi of this task's extrinsic sum in
 // one packed evaluation (RuleMath<kRuleSp32>::pair), the message sign as the

@@ -55,6 +55,7 @@ struct DecodeArgs {
     int clamp_on;
     float ms_scale;    // kRuleMinSum normalisation
     float ms_offset;   // kRuleMinSum offset (subtracted after the scale, floored at 0)
+    int ms_sc;         // kRuleMinSumLds: self-corrected (QKD_MINSUM_SELF_CORRECT)
     // kModeLlr
     const double* llr;
     const uint8_t* syn;
@@ -175,11 +176,12 @@ __host__ __device__ inline int decode_m_words(int m) { return ((m + 63) / 64) * 
 //   ctl    [4]              frame index, block_any flags
 //   cst    [m] (uint4)      kRuleMinSumLds: per-check min-sum state (ms_state)
 struct DecodeLds {
-    size_t tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, cst, bytes;
+    size_t tsyn, xsyn, qsyn, tval, ctab, tab2, t2idx, ctl, cst, czf, bytes;
     // total_esz: bytes per bit total in LDS (0: the totals live in global
-    // memory, large codes)
+    // memory, large codes); cst_checks: min-sum state of that many checks (16
+    // bytes each, and with zf a word of zero flags each, self-corrected min-sum)
     __host__ __device__ DecodeLds(int n_pad, int n_words, int m, int dc, int tab2_entries, int total_esz,
-                                  int cst_checks = 0, int row_esz = 0) {
+                                  int cst_checks = 0, int row_esz = 0, bool zf = false) {
         const int m_words = decode_m_words(m);
         const int esz = row_esz ? row_esz : total_esz;
         tsyn = ((size_t)n_pad * total_esz + 15) & ~(size_t)15;
@@ -195,7 +197,8 @@ struct DecodeLds {
         t2idx = tab2 + (size_t)tab2_entries * 8;
         ctl = (t2idx + (tab2_entries ? (size_t)n_pad * 2 : 0) + 15) & ~(size_t)15;
         cst = ctl + 16;
-        bytes = cst + (size_t)cst_checks * 16;
+        czf = cst + (size_t)cst_checks * 16;
+        bytes = czf + (zf ? (size_t)cst_checks * 4 : 0);
     }
 };
 

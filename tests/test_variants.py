@@ -54,6 +54,9 @@ def test_minsum_model_syndrome_matches_oracle(ms_model, oracle_code):
 
 def test_decoder_flags_validation():
     import qkd_ldpc_amd as Q
+    assert Q.decoder_flags(True, "minsum", minsum_self_correct=True) == 0x1 | 0x20 | (1 << 24)
+    with pytest.raises(ValueError):
+        Q.decoder_flags(True, "sp_f32", minsum_self_correct=True)
     assert Q.decoder_flags(True, "sp_f64") == 0x1
     assert Q.decoder_flags(False, "minsum") == 0x20
     assert Q.decoder_flags(True, "minsum", 0.5) == 0x1 | 0x20 | (128 << 8)
@@ -120,6 +123,45 @@ def test_minsum_llr_bit_exact(Q, H, ms_model, oracle_mod, monkeypatch, store, q,
     assert (r.iterations.cpu().numpy() == want_it).all()
     assert (r.syndromes_match.cpu().numpy() == want_ok).all()
     assert (r.bits.cpu().numpy() == want_bits).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,max_it,thr,thr_on,scale", [
+    (0.05, 50, 100.0, True, None), (0.08, 50, 100.0, True, 0.875), (0.08, 50, 100.0, True, 0.75),
+    (0.07, 6, 2.5, True, 1.0 - 1 / 256), (0.06, 50, 0.0, False, None)])
+def test_minsum_self_corrected_bit_exact(Q, H, ms_model, oracle_mod, q, max_it, thr, thr_on, scale):
+    """Self-corrected min-sum (QKD_MINSUM_SELF_CORRECT, LDS-state kernel) against its
+    specification: erasures of sign-flipped b2c from the second iteration on."""
+    A, B, qq = _frames(oracle_mod, q, 48, seed=int(q * 1000) + 31 + max_it)
+    lp = np.log((1 - qq) / qq)
+    llr = np.where(B == 1, -lp, lp)
+    syn = ms_model.syndrome(A)
+    r = Q.sum_product_decoding(H, _dev(llr, np.float64), _dev(syn, np.uint8), max_it,
+                               thr if thr_on else 100.0, thr_on, variant="minsum",
+                               minsum_scale=scale, minsum_self_correct=True)
+    torch.cuda.synchronize()
+    want_bits, want_it, want_ok = ms_model.decode(llr, syn, max_it, thr, thr_on,
+                                                  0.8125 if scale is None else scale, 0.0, self_correct=True)
+    assert (r.iterations.cpu().numpy() == want_it).all()
+    assert (r.syndromes_match.cpu().numpy() == want_ok).all()
+    assert (r.bits.cpu().numpy() == want_bits).all()
+    # and the keys path
+    r = Q.qkd_ldpc(H, _dev(A, np.uint8), _dev(B, np.uint8), float(qq), max_it,
+                   thr if thr_on else 100.0, thr_on, want_bits=True, variant="minsum",
+                   minsum_scale=scale, minsum_self_correct=True)
+    torch.cuda.synchronize()
+    assert (r.iterations.cpu().numpy() == want_it).all()
+    assert (r.bits.cpu().numpy() == want_bits).all()
+
+
+@pytest.mark.gpu
+def test_minsum_self_corrected_needs_lds_state(Q, H, monkeypatch):
+    """The global-store min-sum has no self-correction: the call fails loudly."""
+    monkeypatch.setenv("QKD_MINSUM_STORE", "global")
+    llr = torch.ones((2, 10240), dtype=torch.float64, device="cuda")
+    syn = torch.zeros((2, 5231), dtype=torch.uint8, device="cuda")
+    with pytest.raises(Q.QkdError):
+        Q.sum_product_decoding(H, llr, syn, 5, 100.0, True, variant="minsum", minsum_self_correct=True)
 
 
 @pytest.mark.gpu
