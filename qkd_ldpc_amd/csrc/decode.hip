@@ -1070,7 +1070,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     // kernel's store.
     const char* kern = getenv("QKD_DECODE_KERNEL");
     const bool classic = kern && !strcmp(kern, "classic");
-    if ((rule == kRuleSp64 || rule == kRuleSp32) && !classic && !a.trace && c->n <= kMaxBitsLds) {
+    if ((rule == kRuleSp64 || rule == kRuleSp32) && !classic && !a.trace && c->n <= kMaxBitsSplit) {
         int sdc = 0;
         DecodeFn sfn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &sdc);
         const int esz = rule == kRuleSp64 ? 8 : 4;
@@ -1079,7 +1079,9 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
         if (const char* b = getenv("QKD_SPLIT_BUDGET")) budget = std::min(budget, (size_t)atol(b));
         const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, esz, budget);
         // (the binary32 rule's kernel keeps every slot in LDS: SplitStore<float, true>)
-        const bool fits = rule == kRuleSp32 ? L.S >= (uint32_t)((size_t)c->max_dv * c->n_pad) : L.S > (uint32_t)c->n;
+        // (binary64: any share of the slots in LDS, the rest in the
+        // workgroup's global region; long codes keep most of them there)
+        const bool fits = rule == kRuleSp32 ? L.S >= (uint32_t)((size_t)c->max_dv * c->n_pad) : L.S >= 64;
         if (L.bytes <= kLdsBytesMax && fits) {
             int grid = 0;
             qkd_status s = decode_grid(c, sfn, L.bytes, &grid);

@@ -228,7 +228,7 @@ constexpr int kSp32Chunk = 3;     // bit-phase rounds per load batch
 template <bool FOLD, int MODE, bool CLAMP, typename MS>
 __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const DecodeArgs& a, const MS& ms,
                                                const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
-                                               uint64_t* zw, uint32_t bobmask, bool keep, uint32_t f, int tid,
+                                               uint64_t* zw, uint64_t bobmask, bool keep, uint32_t f, int tid,
                                                int wave, int lane) {
     const uint32_t n_pad = (uint32_t)c.n_pad;
     const float llr_p = (float)a.log_p;
@@ -255,7 +255,7 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
             int32_t jc[kDvUnroll];
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k) jc[k] = (int32_t)(bc[u] >> (16 * k)) & 0xffff;
-            const uint32_t bob = (bobmask >> r) & 1u;
+            const uint32_t bob = (uint32_t)(bobmask >> r) & 1u;
             float acc;
             if constexpr (MODE == kModeLlr) acc = ok ? (float)a.llr[(size_t)f * c.n + i] : 0.0f;
             else acc = bob ? -llr_p : llr_p;
@@ -500,7 +500,7 @@ constexpr int kIvChunk = QKD_IV_CHUNK;       // rounds per load batch
 template <bool FOLD, int MODE, bool DV3>
 __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const DecodeArgs& a, const SplitStore<double>& ms,
                                                const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
-                                               uint32_t* xunc, uint64_t* zw, uint32_t bobmask, bool keep,
+                                               uint32_t* xunc, uint64_t* zw, uint64_t bobmask, bool keep,
                                                uint32_t f, int tid, int wave, int lane) {
     using qkds::f2;
     static_assert(!DV3 || kDvUnroll == 3, "DV3 unrolls three rows");
@@ -533,7 +533,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             int32_t jc[kDvUnroll];
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k) jc[k] = (int32_t)(bc[u] >> (16 * k)) & 0xffff;
-            const uint32_t bob = (bobmask >> r) & 1u;
+            const uint32_t bob = (uint32_t)(bobmask >> r) & 1u;
             bool z, unc = false;
             f2 bo[kDvUnroll];
             if (FOLD) {
@@ -735,11 +735,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             __syncthreads();
         }
         // Bob's bits of this thread's bit-phase rounds (round r: bit tid + r *
-        // kDecodeBlock; N <= 32 * kDecodeBlock, kMaxBitsLds). Without the fold
+        // kDecodeBlock; N <= 64 * kDecodeBlock, kMaxBitsSplit). Without the fold
         // the first check phase reads b2c = LLR_i (:188) from every slot.
         // (the speculative kernel's replay policy for this frame: ctl[6])
         const bool spec0 = SPEC == 1 && ctl[6] != 0;
-        uint32_t bobmask = 0;
+        uint64_t bobmask = 0;
         // the first check phase's b2c = LLR_i in every slot (:188), as enclosing
         // intervals when speculating (the LLR path has no folded first iteration)
         auto init_slots = [&](bool as_interval) {
@@ -750,7 +750,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     l = (T)a.llr[(size_t)f * c.n + i];
                 } else {
                     const uint32_t bb = (uint32_t)((bw[i >> 6] >> (i & 63)) & 1u);
-                    bobmask |= bb << r;
+                    bobmask |= (uint64_t)bb << r;
                     l = bb ? -llr_p : llr_p;
                 }
                 if (!fold1) {
@@ -904,11 +904,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     const int deg = dg[u];
                     T acc;
                     if (MODE == kModeLlr) acc = ok ? (T)a.llr[(size_t)f * c.n + i] : (T)0;
-                    else acc = ((bobmask >> r) & 1u) ? -llr_p : llr_p;
+                    else acc = ((uint32_t)(bobmask >> r) & 1u) ? -llr_p : llr_p;
                     if constexpr (FOLDS) if (folded && ok) {
                         // fold_first_message: message of the k-th check j of bit i is
                         // +-C_{d_j} with sign = sign(P_j) ^ sign(LLR_i) (first_check_phase)
-                        const uint32_t sgi = ((bobmask >> r) & 1u) ^ lsign;
+                        const uint32_t sgi = ((uint32_t)(bobmask >> r) & 1u) ^ lsign;
 #pragma unroll
                         for (int k = 0; k < kDvUnroll; ++k) {
                             if (k < deg) {
@@ -939,7 +939,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     if (TABLES && folded && tab2_on) {
                         // second_table_index: Bob's bit and the signs of the first
                         // messages; the slot of row k keeps the index of its entry
-                        uint32_t code = (bobmask >> r) & 1u;
+                        uint32_t code = (uint32_t)(bobmask >> r) & 1u;
 #pragma unroll
                         for (int k = 0; k < kTab2MaxDv; ++k)
                             if (k < deg) code |= ((uint32_t)qkdm::hi32(v[u][k]) >> 31) << (1 + k);

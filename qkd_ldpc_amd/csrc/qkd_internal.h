@@ -25,6 +25,9 @@ __host__ __device__ inline int tab2_stride(int max_dv) { return (1 << (1 + max_d
 constexpr int kMaxCheckDegree = 64;
 // The per-frame bit totals live in LDS as binary64: N <= this.
 constexpr int kMaxBitsLds = 20480;
+// The split-store kernels (decode_split.hip): Bob's bits of a thread's
+// bit-phase rounds in one 64-bit register, 64 rounds of kDecodeBlock bits
+constexpr int kMaxBitsSplit = 64 * 1024;
 // Parallel key generation: 64 lanes per frame, jump levels log2(64); frames
 // with more flipped positions than this take the serial kernel.
 constexpr int kKeygenLanes = 64;

@@ -1,8 +1,12 @@
-"""Codes longer than the LDS-resident totals allow (N > 20480): the same decoder
-with its bit totals in global scratch (decode_kernel<..., GT = true>). Random
-regular (3, 6) codes; parity with the oracle bit for bit, fused trials
-included (both key generators: the jump-ahead one for floor(N q) <= 4096 and
-the serial one beyond)."""
+"""Codes longer than the LDS-resident totals allow (N > 20480). The reference's
+binary64 rule runs in the split-store kernel (decode_split.hip: a share of the
+message slots in LDS, the rest in the workgroup's global region, up to N =
+65536), speculative interval iterations included; the classic kernel with its
+bit totals in global scratch (decode_kernel<..., GT = true>) stays behind
+QKD_DECODE_KERNEL=classic and for longer codes. Random regular (3, 6) codes;
+parity with the oracle bit for bit for both kernels, fused trials included
+(both key generators: the jump-ahead one for floor(N q) <= 4096 and the serial
+one beyond)."""
 import numpy as np
 import pytest
 
@@ -79,8 +83,11 @@ def big_codes(big, Q, oracle_mod, tmp_path_factory):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["split", "classic"])
 @pytest.mark.parametrize("q,thr,thr_on", [(0.03, 100.0, True), (0.06, 2.5, True), (0.04, 0.0, False)])
-def test_large_code_decode_bit_exact(Q, big_codes, oracle_mod, q, thr, thr_on):
+def test_large_code_decode_bit_exact(Q, big_codes, oracle_mod, monkeypatch, kernel, q, thr, thr_on):
+    if kernel == "classic":
+        monkeypatch.setenv("QKD_DECODE_KERNEL", "classic")
     H, oc = big_codes
     n = H.num_bit_nodes
     frames = []
@@ -101,10 +108,13 @@ def test_large_code_decode_bit_exact(Q, big_codes, oracle_mod, q, thr, thr_on):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("q", [0.03, 0.11])
-def test_large_code_trials_equal_oracle(Q, big_codes, oracle_mod, q):
+@pytest.mark.parametrize("kernel", ["split", "classic"])
+@pytest.mark.parametrize("q", [0.03, 0.05, 0.11])
+def test_large_code_trials_equal_oracle(Q, big_codes, oracle_mod, monkeypatch, kernel, q):
     """Fused trials (keygen + decode + compare); at q = 0.11 floor(N q) = 4400
     flips take the serial key generator."""
+    if kernel == "classic":
+        monkeypatch.setenv("QKD_DECODE_KERNEL", "classic")
     H, oc = big_codes
     seeds = oracle_mod.seeds(777, 8)
     r = Q.run_trials(H, torch.from_numpy(seeds.view(np.int64)).cuda(), q, 0, 40)
