@@ -10,7 +10,7 @@ cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/r02prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-VARIANTS=${VARIANTS:-"sp_f64 sp_f32 minsum"}
+VARIANTS=${VARIANTS:-"sp_f64 sp_f32 minsum minsum_sc"}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
   python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e > "$OUT/trace.log" 2>&1 \
   || { tail -n 20 "$OUT/trace.log"; exit 3; }
