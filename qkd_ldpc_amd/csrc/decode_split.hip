@@ -37,6 +37,29 @@
 
 namespace qkd {
 
+// The weight of row entry k in the extrinsic sum of a lane at position p
+// (= lane - start) of a segment of degree deg (qkd_decode.h seg_weight_entries).
+template <int DC>
+struct SegWeights {
+    const float* w;         // DC <= 8: wtab row of (deg, p)
+    uint32_t mask;          // otherwise: bit k = weight of entry k
+    __device__ __forceinline__ SegWeights(const float* wtab, int deg, int p) {
+        if constexpr (DC <= 8) {
+            // (idle lanes: a degree-1 segment starting at lane 0, p = lane;
+            // any p >= 1 gives their only weight, entry 0)
+            w = wtab + ((deg - 1) * DC + min(p, DC - 1)) * DC;
+            mask = 0;
+        } else {
+            w = nullptr;
+            mask = ((1u << deg) - 1u) & ~(1u << (uint32_t)p);
+        }
+    }
+    __device__ __forceinline__ float operator[](int k) const {
+        if constexpr (DC <= 8) return w[k];
+        else return (float)((mask >> k) & 1u);
+    }
+};
+
 // One workgroup's message slots: x < S in LDS, the rest in global memory
 // through a buffer descriptor. Every access issues both an LDS and a buffer
 // instruction and selects: lanes whose slot is in LDS give the buffer an
@@ -173,8 +196,8 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
 // spec_check_phase_paired.
 template <bool CLAMP, int DC, typename MS>
 __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan, const uint32_t* tsyn,
-                                                 const MS& ms, float* row, int n_tasks, uint32_t n_pad,
-                                                 float thr, int wave, int lane) {
+                                                 const MS& ms, float* row, const float* wtab, int n_tasks,
+                                                 uint32_t n_pad, float thr, int wave, int lane) {
     constexpr int NW = kDecodeBlock / 64;
     int t = wave;
     if (t >= n_tasks) return;
@@ -195,10 +218,10 @@ __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan,
         wave_lds_sync();
         const int start = pw_start(wt);
         const int deg = pw_deg(wt);
-        const uint32_t wmask = ((1u << deg) - 1u) & ~(1u << (uint32_t)(lane - start));
+        const SegWeights<DC> wk(wtab, deg, lane - start);
         float S = 0.0f;
 #pragma unroll
-        for (int k = 0; k < DC; ++k) S = __builtin_fmaf(row[start + k], (float)((wmask >> k) & 1u), S);
+        for (int k = 0; k < DC; ++k) S = __builtin_fmaf(row[start + k], wk[k], S);
         const qkds::f2 pv = RuleMath<kRuleSp32>::pair(xn, S);
         const uint32_t j = pw_chk(wt);
         const uint32_t neg = ((tsyn[j >> 5] >> (j & 31)) & 1u) ^
@@ -305,7 +328,8 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
 // the output bound is evaluated per edge. Pipelined as split_check_phase.
 template <int DC>
 __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ plan, const uint32_t* tsyn,
-                                                 const SplitStore<double>& ms, double* row, int n_tasks,
+                                                 const SplitStore<double>& ms, double* row, const float* wtab,
+                                                 int n_tasks,
                                                  uint32_t n_pad, uint32_t n_bits, float thr_dn, float thr_up,
                                                  uint32_t* round_word, int wave, int lane) {
     using qkds::f2;
@@ -337,11 +361,11 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         // the own term would widen the interval by the own term's width)
         // (weight of entry k: bit k of the segment's mask without this lane)
         f2 sum = f2{0.0f, 0.0f};
-        const uint32_t wmask = ((1u << deg) - 1u) & ~(1u << (uint32_t)(lane - start));
+        const SegWeights<DC> wk(wtab, deg, lane - start);
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             const f2 o = qkds::unpack_iv(row[start + k]);
-            sum = __builtin_elementwise_fma(o, f2((float)((wmask >> k) & 1u)), sum);
+            sum = __builtin_elementwise_fma(o, f2(wk[k]), sum);
         }
         // widened by the binary32 roundings (relative to the sum; small
         // buckets charge every segment the bucket's count) and the
@@ -400,7 +424,8 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
 // of their input bound, plan words two.
 template <int DC>
 __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict__ plan, const uint32_t* tsyn,
-                                                        const SplitStore<double>& ms, double* row, int n_tasks,
+                                                        const SplitStore<double>& ms, double* row, const float* wtab,
+                                                        int n_tasks,
                                                         uint32_t n_pad, uint32_t n_bits, float thr_dn, float thr_up,
                                                         uint32_t* round_word, int wave, int lane) {
     using qkds::f2;
@@ -444,11 +469,11 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         const int start = pw_start(wt);
         const int deg = pw_deg(wt);
         f2 sum = f2{0.0f, 0.0f};
-        const uint32_t wmask = ((1u << deg) - 1u) & ~(1u << (uint32_t)(lane - start));
+        const SegWeights<DC> wk(wtab, deg, lane - start);
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             const f2 o = qkds::unpack_iv(row[start + k]);
-            sum = __builtin_elementwise_fma(o, f2((float)((wmask >> k) & 1u)), sum);
+            sum = __builtin_elementwise_fma(o, f2(wk[k]), sum);
         }
         const float nr = DC <= 8 ? (float)(DC + 2) : (float)(deg + 2);
         const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
@@ -650,6 +675,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
     double* tab2 = reinterpret_cast<double*>(smem + L.tab2);
+    float* wtab = reinterpret_cast<float*>(smem + L.wtab);
+    for (int e = threadIdx.x; e < seg_weight_entries(DC); e += kDecodeBlock) {
+        const int k = e % DC, p = (e / DC) % DC, deg = e / (DC * DC) + 1;
+        wtab[e] = (k < deg && k != p) ? 1.0f : 0.0f;
+    }
     using MS = SplitStore<T, RULE == kRuleSp32>;
     const MS ms{
         reinterpret_cast<T*>(smem + L.msg),
@@ -818,18 +848,18 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     // (iteration 2 after the folded first one: the slots hold
                     // the phi bounds of exact b2c, psi_of_exact)
                     if (!folded && fold1 && it == 1) {
-                        spec_check_phase_psi<DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
+                        spec_check_phase_psi<DC>(c.plan, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
                                                    a.thr_up, rw, wave, lane);
                         __syncthreads();
                     } else if (!folded) {
-                        spec_check_phase_paired<DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
+                        spec_check_phase_paired<DC>(c.plan, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
                                                     a.thr_up, rw, wave, lane);
                         __syncthreads();
                     }
                 }
             } else if (!folded) {
                 if constexpr (RULE == kRuleSp32)
-                    sp32_check_phase<CLAMP, DC>(c.plan, tsyn, ms, row, n_tasks, n_pad, thr, wave, lane);
+                    sp32_check_phase<CLAMP, DC>(c.plan, tsyn, ms, row, wtab, n_tasks, n_pad, thr, wave, lane);
                 else if (TABLES && it == 1 && tab2_on)
                     split_check_phase<kSrcTable, CLAMP, DC, RULE>(c.plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);

@@ -428,12 +428,19 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 //   ctab  [kFirstTableDeg + 1]   first-iteration message magnitudes by degree
 //   tab2  [tab2_entries]         second-iteration tanh table
 //   ctl   [8]                    [1] next frame, [4..5] round flags (decode_split.hip)
+//   wtab  [dc][dc][dc] float     extrinsic-sum weights by (degree, position, k) (dc <= 8)
 //   msg   [S + 64] T             message slots 0 .. S-1 (slots S .. max_dv*n_pad-1
 //                                live in the workgroup's global region), then
 //                                one trash slot per lane
 // S is as many slots as the budget leaves after the rest, in whole 64s.
+// Weights of a check phase's extrinsic sums: lane at position p of a
+// segment of degree deg sums row entry k with weight (k < deg && k != p).
+// Buckets up to 8 read them from an LDS table (wtab[deg - 1][p][k], two
+// per ds_read_b64) instead of extracting and converting mask bits per entry.
+__host__ __device__ inline int seg_weight_entries(int dc) { return dc <= 8 ? dc * dc * dc : 0; }
+
 struct SplitLds {
-    size_t tsyn, xsyn, qsyn, xunc, zw, tval, ctab, tab2, ctl, msg, bytes;
+    size_t tsyn, xsyn, qsyn, xunc, zw, tval, ctab, tab2, ctl, wtab, msg, bytes;
     uint32_t S;
     __host__ __device__ SplitLds(int n_pad, int n_words, int m, int max_dv, int dc, int tab2_entries, int esz,
                                  size_t budget) {
@@ -449,7 +456,8 @@ struct SplitLds {
         ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         ctl = (tab2 + (size_t)tab2_entries * 8 + 15) & ~(size_t)15;
-        msg = ctl + 32;
+        wtab = ctl + 32;
+        msg = (wtab + (size_t)seg_weight_entries(dc) * 4 + 15) & ~(size_t)15;
         const size_t slots = (size_t)max_dv * n_pad;
         // 64 trash slots follow the S message slots (decode_split.hip SplitStore)
         const size_t fit = budget > msg + 64 * (size_t)esz ? (budget - msg) / (size_t)esz - 64 : 0;
