@@ -189,7 +189,8 @@ ThreadCtx& ctx() {
 }
 
 // The reference's only decoder switch is the clamp. QKD_AMD_VARIANT=sp_f32 |
-// minsum selects one of the library's binary32 variants for a whole run (the
+// minsum | minsum_sc selects one of the library's binary32 variants for a
+// whole run (the
 // default, sp_f64, is the reference's decoder bit for bit).
 uint32_t variant_from_env() {
     static const uint32_t v = [] {
@@ -197,6 +198,7 @@ uint32_t variant_from_env() {
         if (!e || !*e || !std::strcmp(e, "sp_f64")) return QKD_VARIANT_SP_F64;
         if (!std::strcmp(e, "sp_f32")) return QKD_VARIANT_SP_F32;
         if (!std::strcmp(e, "minsum")) return QKD_VARIANT_MINSUM;
+        if (!std::strcmp(e, "minsum_sc")) return QKD_VARIANT_MINSUM | QKD_MINSUM_SELF_CORRECT | QKD_MINSUM_SCALE(0.875);
         throw std::runtime_error(std::string("QKD_AMD_VARIANT: unknown decoder variant '") + e + "'");
     }();
     return v;

@@ -27,7 +27,7 @@
 // xoshiro256++(simulation_seed) stream (qkd_interactive_batch).
 //
 //   qkd_ldpc_sim [--root DIR] [--config FILE] [--matrix-dir DIR] [--results-dir DIR]
-//                [--gpus N | --devices i,j,...] [--variant sp_f64|sp_f32|minsum]
+//                [--gpus N | --devices i,j,...] [--variant sp_f64|sp_f32|minsum|minsum_sc]
 //                [--dry-run] [--sort-rows] [--quiet]
 //
 // --sort-rows reads alist files whose lines are not ascending (rejected by
@@ -307,10 +307,12 @@ Args parse_args(int argc, char** argv) {
             if (v == "sp_f64") a.variant = QKD_VARIANT_SP_F64;
             else if (v == "sp_f32") a.variant = QKD_VARIANT_SP_F32;
             else if (v == "minsum") a.variant = QKD_VARIANT_MINSUM;
+            // self-corrected min-sum at its best scale
+            else if (v == "minsum_sc") a.variant = QKD_VARIANT_MINSUM | QKD_MINSUM_SELF_CORRECT | QKD_MINSUM_SCALE(0.875);
             else throw std::runtime_error("unknown --variant '" + v + "'");
         } else if (k == "-h" || k == "--help") {
             std::printf("usage: qkd_ldpc_sim [--root DIR] [--config FILE] [--matrix-dir DIR] [--results-dir DIR]\n"
-                        "                    [--gpus N | --devices i,j,...] [--variant sp_f64|sp_f32|minsum]\n"
+                        "                    [--gpus N | --devices i,j,...] [--variant sp_f64|sp_f32|minsum|minsum_sc]\n"
                         "                    [--dry-run] [--sort-rows] [--quiet]\n");
             std::exit(0);
         } else {
