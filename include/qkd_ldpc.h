@@ -266,7 +266,10 @@ QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, con
  * which = 5 takes its interval in log2-domain units (x = S / ln 2).
  * which = 8 / 9: quadruples (a, b, s_lo, s_hi) -> raw binary32 (in lo, in hi,
  * out lo, out hi) of the packed phi_pair (8) and of the scalar phi_bounds +
- * phi_bounds_out it must equal bit for bit (9); n a multiple of 4. */
+ * phi_bounds_out it must equal bit for bit (9); n a multiple of 4.
+ * which = 10 / 11: pairs of exact b2c -> the raw bits of their psi bounds
+ * (two binary32 per output double) from the packed psi_of_exact2 (10) and
+ * the scalar psi_of_exact (11); n even. */
 QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
 /* Exhaustive check of the speculative iterations' phi bounds (qkd_spec.h) at
  * EVERY binary32 a with bit pattern in [first_bits, last_bits] (positive

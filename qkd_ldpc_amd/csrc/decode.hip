@@ -1599,6 +1599,23 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
             y[i + 3] = out.y;
             break;
         }
+        case 10:
+        case 11: {
+            // pairs of exact b2c (x[2k], x[2k+1]) -> raw binary32 psi bounds
+            // (lo, hi of each): 10 the packed qkds::psi_of_exact2, 11 the
+            // scalar psi_of_exact twice; one thread per pair
+            if (i & 1) break;
+            qkds::f2 r0, r1;
+            if (which == 10) {
+                qkds::psi_of_exact2(x[i], x[i + 1], r0, r1);
+            } else {
+                r0 = qkds::psi_of_exact(x[i]);
+                r1 = qkds::psi_of_exact(x[i + 1]);
+            }
+            y[i] = __builtin_bit_cast(double, r0);
+            y[i + 1] = __builtin_bit_cast(double, r1);
+            break;
+        }
         case 6: y[i] = (double)__builtin_amdgcn_exp2f((float)x[i]); break;   // hardware v_exp_f32
         case 7: y[i] = (double)__builtin_amdgcn_logf((float)x[i]); break;    // hardware v_log_f32
         default: y[i] = (double)RuleMath<kRuleSp32>::two_atanh((float)x[i]); break;  // phi(S ln 2)
@@ -1607,7 +1624,8 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
 
 qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void* stream) {
     clear_error();
-    if (!x || !y || which < 0 || which > 9) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if (!x || !y || which < 0 || which > 11) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if ((which == 10 || which == 11) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "psi pairs take n even");
     if ((which == 4 || which == 5) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "phi bounds take pairs (n even)");
     if ((which == 8 || which == 9) && (n & 3))
         return set_error(QKD_ERR_INVALID_ARG, "paired phi bounds take quadruples (n % 4 == 0)");

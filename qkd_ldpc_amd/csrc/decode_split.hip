@@ -576,8 +576,9 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) acc = (DV3 || k < deg) ? acc + cv[k] : acc;
                 z = ok && acc <= 0;
-#pragma unroll
-                for (int k = 0; k < kDvUnroll; ++k) bo[k] = qkds::psi_of_exact(clamp_msg(acc - cv[k], a.thr));
+                static_assert(kDvUnroll == 3, "rows 0 and 1 paired, row 2 alone");
+                qkds::psi_of_exact2(clamp_msg(acc - cv[0], a.thr), clamp_msg(acc - cv[1], a.thr), bo[0], bo[1]);
+                bo[2] = qkds::psi_of_exact(clamp_msg(acc - cv[2], a.thr));
             } else {
                 f2 L;
                 if constexpr (MODE == kModeLlr) L = qkds::iv_of(ok ? a.llr[(size_t)f * c.n + i] : 0.0);

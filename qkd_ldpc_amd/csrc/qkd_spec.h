@@ -155,6 +155,7 @@ struct PhiVal2 {
     f2 v;
     f2 slope;
 };
+template <bool PSI1 = false>   // half 1 in psi units too
 __device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u) {
     f2 t = __builtin_elementwise_fma(x, f2(1.0f / 5040.0f), f2(-1.0f / 720.0f));
     t = __builtin_elementwise_fma(x, t, f2(1.0f / 120.0f));
@@ -169,7 +170,7 @@ __device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u) {
     const f2 rw = f2{__builtin_amdgcn_rcpf(w.x), __builtin_amdgcn_rcpf(w.y)};
     const f2 arg = w2 * rw;
     const float lg1 = __builtin_amdgcn_logf(arg.y);
-    const f2 vlo = f2{__builtin_amdgcn_logf(arg.x), kLn2 * lg1};
+    const f2 vlo = f2{__builtin_amdgcn_logf(arg.x), PSI1 ? lg1 : kLn2 * lg1};
     const f2 s = u * u;
     f2 h = __builtin_elementwise_fma(s, f2(1.0f / 13.0f), f2(1.0f / 11.0f));
     h = __builtin_elementwise_fma(s, h, f2(1.0f / 9.0f));
@@ -177,7 +178,7 @@ __device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u) {
     h = __builtin_elementwise_fma(s, h, f2(0.2f));
     h = __builtin_elementwise_fma(s, h, f2(1.0f / 3.0f));
     h = __builtin_elementwise_fma(s, h, f2(1.0f));
-    const f2 vhi = (u * f2{2.0f * kInvLn2, 2.0f}) * h;
+    const f2 vhi = (u * f2{2.0f * kInvLn2, PSI1 ? 2.0f * kInvLn2 : 2.0f}) * h;
     PhiVal2 o;
     o.v = f2{x.x < 1.0f ? vlo.x : vhi.x, x.y < 1.0f ? vlo.y : vhi.y};
     o.slope = (f2(2.0f) * u) * rw;
@@ -238,6 +239,32 @@ __device__ __forceinline__ f2 psi_of_exact(double b) {
     const bool ok = (neg || iv.x > 0.0f) && ab.x > 1.0e-30f;
     const f2 ph = phi_bounds(ab.x, ab.y);
     return ok ? (neg ? -ph.yx : ph) : f2{__builtin_nanf(""), __builtin_nanf("")};
+}
+
+// psi_of_exact of two values in one packed evaluation (phi_bounds' operations
+// in each half: bit for bit psi_of_exact of each).
+__device__ __forceinline__ void psi_of_exact2(double b0, double b1, f2& r0, f2& r1) {
+    const f2 i0 = iv_of(b0), i1 = iv_of(b1);
+    const bool n0 = i0.y < 0.0f, n1 = i1.y < 0.0f;
+    const f2 a0 = n0 ? -i0.yx : i0, a1 = n1 ? -i1.yx : i1;
+    const bool ok0 = (n0 || i0.x > 0.0f) && a0.x > 1.0e-30f;
+    const bool ok1 = (n1 || i1.x > 0.0f) && a1.x > 1.0e-30f;
+    // phi_bounds(a.x, a.y) in both halves: exp_neg's argument split, phi_core
+    const f2 x = f2{__builtin_amdgcn_fmed3f(a0.x, 0.0f, kPhiHuge), __builtin_amdgcn_fmed3f(a1.x, 0.0f, kPhiHuge)};
+    const float L = 1.44269502162933349609375f;
+    const float L_lo = 1.925963033500011079e-08f;
+    const f2 p = x * f2(L);
+    const f2 rl = __builtin_elementwise_fma(__builtin_elementwise_fma(x, f2(L), -p), f2(kLn2), x * f2(L_lo * kLn2));
+    const f2 e2 = f2{__builtin_amdgcn_exp2f(-p.x), __builtin_amdgcn_exp2f(-p.y)};
+    const f2 u = __builtin_elementwise_fma(e2, -rl, e2);
+    const PhiVal2 e = phi_core_pair<true>(x, u);
+    const f2 hi = __builtin_elementwise_fma(e.v, f2(kPhiRel), e.v) + f2(1.0e-37f);
+    const f2 t = __builtin_elementwise_fma(-e.slope * f2((1.0f + 2.0f * kPhiRel) * kInvLn2), f2{a0.y, a1.y} - x,
+                                           e.v * f2(1.0f - kPhiRel));
+    const f2 ph0 = f2{t.x > 0.0f ? t.x : 0.0f, hi.x}, ph1 = f2{t.y > 0.0f ? t.y : 0.0f, hi.y};
+    const float nan = __builtin_nanf("");
+    r0 = ok0 ? (n0 ? -ph0.yx : ph0) : f2{nan, nan};
+    r1 = ok1 ? (n1 ? -ph1.yx : ph1) : f2{nan, nan};
 }
 
 // An interval travels through the double-width message slots as its bits.

@@ -414,3 +414,25 @@ def test_spec_llr_path_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypa
     assert torch.equal(sp.iterations, ex.iterations)
     assert torch.equal(sp.syndromes_match, ex.syndromes_match)
     assert torch.equal(sp.bits, ex.bits)
+
+
+def test_psi_of_exact_pair_equals_scalar(Q):
+    """The folded bit phase's packed psi bounds of two exact b2c (psi_of_exact2) equal
+    the scalar psi_of_exact bit for bit, special values included (0, +-0, NaN, +-inf,
+    the clamp, subnormal and tiny magnitudes, the branch edges)."""
+    rng = np.random.default_rng(19)
+    n = 1 << 20
+    x = np.exp(rng.uniform(np.log(1e-35), np.log(150.0), n)) * rng.choice([-1.0, 1.0], n)
+    special = np.array([0.0, -0.0, np.nan, np.inf, -np.inf, 100.0, -100.0, 1e-30, -1e-30, 1e-31, 5e-324,
+                        0.35, 1.0, 80.0, 2.0, -0.35, np.nextafter(0.35, 0), np.nextafter(1.0, 0)])
+    x[: special.size] = special
+    x[special.size: 2 * special.size] = special[::-1]
+    dx = torch.from_numpy(x).cuda()
+    out = {}
+    for which in (10, 11):
+        dy = torch.empty_like(dx)
+        Q._native.check(Q._native.lib().qkd_debug_math(which, dx.data_ptr(), dy.data_ptr(), dx.numel(), None))
+        torch.cuda.synchronize()
+        out[which] = dy.cpu().numpy().view(np.uint64)
+    bad = np.nonzero(out[10] != out[11])[0]
+    assert bad.size == 0, (bad[:8], x[bad[:8]])
