@@ -216,8 +216,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # one process per GPU over RCCL ("nccl"); QKD_DIST_BACKEND=gloo with more
+        # ranks than GPUs rehearses the multi-rank path on one device (tests)
+        backend = os.environ.get("QKD_DIST_BACKEND", "nccl")
+        if backend != "nccl":
+            local %= torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     import qkd_ldpc_amd as Q
 
     H, g = load_code(torch.cuda.current_device())
