@@ -679,40 +679,48 @@ __global__ void keygen_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n
     if (exact_q) exact_q[f] = (double)ne / (double)n;
 }
 
-// ---- key generation: one wave per frame (jump-ahead) --------------------------
-// Same key pair as keygen_kernel, drawn in parallel. The trial's draw stream
-// (qkdr::trial_draws) is cut into 64 chunks of `chunk` draws; lane l jumps the
-// seeded state by l * chunk draws (jump[b] = T^(chunk * 2^b), applied for the
-// set bits of l) and then steps through its chunk:
+// ---- key generation: kKeygenLanes lanes per frame (jump-ahead) ---------------
+// Same key pair as keygen_kernel, drawn in parallel; kKeygenFrames frames per
+// workgroup, each on its own kKeygenLanes-lane slice of it. The
+// trial's draw stream (qkdr::trial_draws) is cut into kKeygenLanes chunks of
+// `chunk` draws; lane l of a frame jumps the seeded state by l * chunk draws
+// (jump[b] = T^(chunk * 2^b), applied for the set bits of l: a jump is a
+// 256x256 GF(2) product per level and lane, so fewer lanes per frame mean fewer
+// levels and less work per frame) and then steps through its chunk:
 //   draws [0, N)      Alice's bits (whole words per lane: chunk % 64 == 0)
 //   draw N (even N)   the lone swap of std::shuffle
 //   the rest          one Lemire draw per shuffle pair (i, i+1)
 // Shuffle steps with index < ne need the exact swap sequence: their draws are
-// parked in LDS and replayed by lane 0 (qkdr::shuffle_low_positions, steps
-// i < ne). Steps >= ne only ever write "low[x] = i", so the last such writer
-// of each low position is found with an LDS atomicMax. A Lemire rejection
+// parked in LDS and replayed by the frame's lane 0 (qkdr::shuffle_low_positions,
+// steps i < ne). Steps >= ne only ever write "low[x] = i", so the last such
+// writer of each low position is found with an LDS atomicMax. A Lemire rejection
 // (probability ~ range / 2^64 per draw) shifts every later draw: such a frame
-// is regenerated serially by lane 0 from its seed.
-__global__ __launch_bounds__(64) void keygen_fast_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
+// is regenerated serially by its lane 0 from its seed.
+__global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
                                                          uint32_t words, uint32_t ne, uint32_t chunk,
-                                                         const uint64_t* __restrict__ jump, uint64_t* alice_w,
-                                                         uint64_t* bob_w, double* exact_q,
+                                                         uint32_t n_frames, const uint64_t* __restrict__ jump,
+                                                         uint64_t* alice_w, uint64_t* bob_w, double* exact_q,
                                                          uint32_t force_serial) {
     extern __shared__ uint32_t kg_lds[];
-    uint32_t* low = kg_lds;                          // ne: replayed positions
-    uint32_t* last = low + ne;                       // ne: last step >= ne writing here (0 = none)
-    uint2* park = (uint2*)(last + ne + (ne & 1u));   // ne / 2 + 1 parked pair draws
-    __shared__ uint32_t s_lone, s_reject;
+    __shared__ uint32_t s_lone[kKeygenFrames], s_reject[kKeygenFrames];
+    const uint32_t slot = threadIdx.x / kKeygenLanes;          // this frame's slice of the workgroup
+    const uint32_t lane = threadIdx.x % kKeygenLanes;
+    // per frame (an even number of words, so every park is 8-byte aligned):
+    // low[ne], last[ne], park[ne / 2 + 1]
+    const uint32_t frame_words = 2 * ne + 2 * (ne / 2 + 1);
+    uint32_t* low = kg_lds + (size_t)slot * frame_words;     // ne: replayed positions
+    uint32_t* last = low + ne;                               // ne: last step >= ne writing here (0 = none)
+    uint2* park = (uint2*)(last + ne);                       // ne / 2 + 1 parked pair draws
 
-    const uint32_t f = blockIdx.x;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t f = blockIdx.x * kKeygenFrames + slot;
+    const bool live = f < n_frames;                          // (the last workgroup may hold fewer frames)
     const bool even = (n & 1u) == 0;
     const uint64_t pair0 = even ? (uint64_t)n + 1 : (uint64_t)n;  // draw index of the first pair
     const uint32_t i0 = even ? 2u : 1u;                             // its step index
     const uint64_t draws = qkdr::trial_draws(n);
 
     qkdr::Xoshiro256pp g;
-    g.seed(seeds[f] + offset);
+    g.seed(live ? seeds[f] + offset : 0);
     uint64_t st[4] = {g.s0, g.s1, g.s2, g.s3};
     for (int b = 0; b < kKeygenLevels; ++b) {
         uint64_t t[4] = {st[0], st[1], st[2], st[3]};
@@ -723,20 +731,20 @@ __global__ __launch_bounds__(64) void keygen_fast_kernel(const uint64_t* seeds, 
     }
     g.s0 = st[0]; g.s1 = st[1]; g.s2 = st[2]; g.s3 = st[3];
 
-    for (uint32_t p = lane; p < ne; p += 64) {
+    for (uint32_t p = lane; p < ne; p += kKeygenLanes) {
         low[p] = p;
         last[p] = 0;
     }
     if (lane == 0) {
-        s_lone = 0;
-        s_reject = force_serial;
+        s_lone[slot] = 0;
+        s_reject[slot] = force_serial;
     }
     __syncthreads();
 
     uint64_t* A = alice_w + (size_t)f * words;
     uint64_t* B = bob_w + (size_t)f * words;
     const uint64_t first = (uint64_t)lane * chunk;
-    const uint64_t end = min(first + chunk, draws);
+    const uint64_t end = live ? min(first + chunk, draws) : first;
     uint64_t acc = 0;
     for (uint64_t d = first; d < end; ++d) {
         const uint64_t r = g.next();
@@ -748,13 +756,13 @@ __global__ __launch_bounds__(64) void keygen_fast_kernel(const uint64_t* seeds, 
                 acc = 0;
             }
         } else if (d < pair0) {
-            s_lone = (uint32_t)(r >> 63);
+            s_lone[slot] = (uint32_t)(r >> 63);
         } else {
             const uint32_t i = i0 + 2u * (uint32_t)(d - pair0);
             const uint64_t b1 = (uint64_t)i + 2;
             const uint64_t range = ((uint64_t)i + 1) * b1;
             const uint64_t lo = r * range;
-            if (lo < range && lo < (0 - range) % range) s_reject = 1;
+            if (lo < range && lo < (0 - range) % range) s_reject[slot] = 1;
             const uint64_t x = qkdr::mul_hi64(r, range);
             // quotient through binary64, corrected to the exact integer one
             uint64_t a = (uint64_t)((double)x / (double)b1);
@@ -772,7 +780,7 @@ __global__ __launch_bounds__(64) void keygen_fast_kernel(const uint64_t* seeds, 
     }
     __syncthreads();
 
-    if (s_reject) {
+    if (live && s_reject[slot]) {
         // exact serial regeneration of this frame (never observed in practice)
         if (lane == 0) {
             qkdr::Xoshiro256pp h;
@@ -788,10 +796,7 @@ __global__ __launch_bounds__(64) void keygen_fast_kernel(const uint64_t* seeds, 
             for (uint32_t p = 0; p < ne; ++p) B[low[p] >> 6] ^= 1ull << (low[p] & 63);
             if (exact_q) exact_q[f] = (double)ne / (double)n;
         }
-        return;
-    }
-
-    if (lane == 0) {
+    } else if (live && lane == 0) {
         // replay of the steps with index < ne (shuffle_low_positions' step())
         auto step = [&](uint32_t si, uint32_t x) {
             if (si < ne) {
@@ -803,7 +808,7 @@ __global__ __launch_bounds__(64) void keygen_fast_kernel(const uint64_t* seeds, 
             }
         };
         if (n > 1) {
-            if (even) step(1, s_lone);
+            if (even) step(1, s_lone[slot]);
             for (uint32_t i = i0; i < ne && i < n; i += 2) {
                 const uint2 q = park[(i - i0) >> 1];
                 step(i, q.x);
@@ -813,9 +818,11 @@ __global__ __launch_bounds__(64) void keygen_fast_kernel(const uint64_t* seeds, 
         if (exact_q) exact_q[f] = (double)ne / (double)n;
     }
     __syncthreads();
-    for (uint32_t p = lane; p < ne; p += 64) {
-        const uint32_t pos = last[p] ? last[p] : low[p];
-        atomicXor((unsigned long long*)&B[pos >> 6], 1ull << (pos & 63));
+    if (live && !s_reject[slot]) {
+        for (uint32_t p = lane; p < ne; p += kKeygenLanes) {
+            const uint32_t pos = last[p] ? last[p] : low[p];
+            atomicXor((unsigned long long*)&B[pos >> 6], 1ull << (pos & 63));
+        }
     }
 }
 
@@ -1413,10 +1420,10 @@ static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uin
     const bool serial = mode && !strcmp(mode, "serial");
     const uint32_t replay = mode && !strcmp(mode, "replay") ? 1u : 0u;
     if (ne <= kKeygenFastMaxErrors && c->d_jump && !serial) {
-        const size_t lds = (2 * (size_t)ne + (ne & 1u)) * sizeof(uint32_t) + (ne / 2 + 1) * sizeof(uint2);
-        hipLaunchKernelGGL(keygen_fast_kernel, dim3((unsigned)n_frames), dim3(kKeygenLanes), lds, stream, seeds,
-                           offset, (uint32_t)c->n, words, (uint32_t)ne, c->keygen_chunk, c->d_jump, ws->alice_w,
-                           ws->bob_w, exact_q, replay);
+        const size_t lds = (size_t)kKeygenFrames * (2 * (size_t)ne * sizeof(uint32_t) + (ne / 2 + 1) * sizeof(uint2));
+        hipLaunchKernelGGL(keygen_fast_kernel, dim3((unsigned)((n_frames + kKeygenFrames - 1) / kKeygenFrames)),
+                           dim3(kKeygenBlock), lds, stream, seeds, offset, (uint32_t)c->n, words, (uint32_t)ne,
+                           c->keygen_chunk, (uint32_t)n_frames, c->d_jump, ws->alice_w, ws->bob_w, exact_q, replay);
     } else {
         hipLaunchKernelGGL(keygen_kernel, dim3(blocks_for(n_frames, 64)), dim3(64), 0, stream, seeds, offset,
                            (uint32_t)n_frames, (uint32_t)c->n, words, (uint32_t)ne, ws->alice_w, ws->bob_w,

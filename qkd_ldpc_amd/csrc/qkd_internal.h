@@ -30,8 +30,15 @@ constexpr int kMaxBitsLds = 20480;
 constexpr int kMaxBitsSplit = 64 * 1024;
 // Parallel key generation: 64 lanes per frame, jump levels log2(64); frames
 // with more flipped positions than this take the serial kernel.
-constexpr int kKeygenLanes = 64;
-constexpr int kKeygenLevels = 6;
+// keygen_fast_kernel: kKeygenLanes lanes per frame (kKeygenLevels = log2 of
+// it jump levels), kKeygenFrames frames per workgroup of kKeygenBlock threads
+#ifndef QKD_KEYGEN_LEVELS
+#define QKD_KEYGEN_LEVELS 6
+#endif
+constexpr int kKeygenLevels = QKD_KEYGEN_LEVELS;
+constexpr int kKeygenLanes = 1 << kKeygenLevels;
+constexpr int kKeygenBlock = kKeygenLanes < 64 ? 64 : kKeygenLanes;   // threads per workgroup
+constexpr int kKeygenFrames = kKeygenBlock / kKeygenLanes;
 constexpr uint32_t kKeygenFastMaxErrors = 4096;
 
 // Device-resident, immutable view of H.
@@ -128,7 +135,8 @@ struct qkd_code {
     uint64_t* d_bit_code = nullptr;
     uint8_t* d_pat_deg = nullptr;
     // parallel key generation (decode.hip: keygen_fast_kernel): lane l of a
-    // frame's wave starts at draw l * keygen_chunk; d_jump[b] = T^(chunk * 2^b)
+    // frame's kKeygenLanes-lane slice starts at draw l * keygen_chunk;
+    // d_jump[b] = T^(chunk * 2^b)
     uint32_t keygen_chunk = 0;
     uint64_t* d_jump = nullptr;
     int cu_count = 0;
