@@ -269,7 +269,10 @@ QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, con
  * phi_bounds_out it must equal bit for bit (9); n a multiple of 4.
  * which = 10 / 11: pairs of exact b2c -> the raw bits of their psi bounds
  * (two binary32 per output double) from the packed psi_of_exact2 (10) and
- * the scalar psi_of_exact (11); n even. */
+ * the scalar psi_of_exact (11); n even.
+ * which = 12 / 13: pairs (x, S) -> (|sign(x) phi(|x|) / ln 2|, phi(S ln 2))
+ * of the binary32 variant, from its packed evaluation (12) and from the
+ * scalar forms of which = 2 / 3 (13), which must agree bit for bit; n even. */
 QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
 /* Exhaustive check of the speculative iterations' phi bounds (qkd_spec.h) at
  * EVERY binary32 a with bit pattern in [first_bits, last_bits] (positive

@@ -1623,6 +1623,22 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
             y[i + 1] = __builtin_bit_cast(double, r1);
             break;
         }
+        case 12:
+        case 13: {
+            // pairs (x, S) -> (|tanh_half(x)|, two_atanh(S)) of the binary32 rule:
+            // 12 the packed RuleMath<kRuleSp32>::pair, 13 the scalar forms
+            if (i & 1) break;
+            qkds::f2 r;
+            if (which == 12) {
+                r = RuleMath<kRuleSp32>::pair((float)x[i], (float)x[i + 1]);
+            } else {
+                r = qkds::f2{__builtin_fabsf(RuleMath<kRuleSp32>::tanh_half((float)x[i])),
+                             RuleMath<kRuleSp32>::two_atanh((float)x[i + 1])};
+            }
+            y[i] = r.x;
+            y[i + 1] = r.y;
+            break;
+        }
         case 6: y[i] = (double)__builtin_amdgcn_exp2f((float)x[i]); break;   // hardware v_exp_f32
         case 7: y[i] = (double)__builtin_amdgcn_logf((float)x[i]); break;    // hardware v_log_f32
         default: y[i] = (double)RuleMath<kRuleSp32>::two_atanh((float)x[i]); break;  // phi(S ln 2)
@@ -1631,8 +1647,9 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
 
 qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void* stream) {
     clear_error();
-    if (!x || !y || which < 0 || which > 11) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if (!x || !y || which < 0 || which > 13) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
     if ((which == 10 || which == 11) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "psi pairs take n even");
+    if ((which == 12 || which == 13) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "rule pairs take n even");
     if ((which == 4 || which == 5) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "phi bounds take pairs (n even)");
     if ((which == 8 || which == 9) && (n & 3))
         return set_error(QKD_ERR_INVALID_ARG, "paired phi bounds take quadruples (n % 4 == 0)");

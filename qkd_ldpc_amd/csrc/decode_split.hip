@@ -227,9 +227,10 @@ __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan,
         const uint32_t neg = ((tsyn[j >> 5] >> (j & 31)) & 1u) ^
                              (uint32_t)(DC <= 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^
                              (neg_t ? 1u : 0u);
-        float v = neg ? -pv.y : pv.y;
-        if (CLAMP) v = clamp_msg(v, thr);
-        ms.st(slot(wt), v);
+        // pv.y is never NaN (the sum enters through fminf), so clamp_msg of
+        // +-pv.y is +-min(pv.y, thr) (thr > 0: check_decode_params)
+        const float m = CLAMP ? __builtin_fminf(pv.y, thr) : pv.y;
+        ms.st(slot(wt), neg ? -m : m);
         row[lane] = pv.x;
         sgn_t = __ballot(xn < 0.0f);
         neg_t = xn < 0.0f;
@@ -307,7 +308,9 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
             for (int k = 0; k < kDvUnroll; ++k) {
                 if (k < deg) {
                     float b = acc - v[u][k];
-                    if (CLAMP) b = clamp_msg(b, thr);
+                    // keys path: b is finite (LLR +-log_p, clamped messages), where
+                    // v_med3_f32 is clamp_msg exactly; LLR input may carry NaN
+                    if (CLAMP) b = MODE == kModeKeys ? __builtin_amdgcn_fmed3f(b, -thr, thr) : clamp_msg(b, thr);
                     ms.st((uint32_t)k * n_pad + i, b);
                 }
             }
