@@ -143,8 +143,7 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
     int t = wave;
     if (t >= n_tasks) return;
     const uint2* pl = plan + lane;
-    // n_pad < 2^24 and rows < 32: a 24-bit multiply
-    auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
+    auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
     auto sbit = [&](uint2 p) -> uint32_t {
         const uint32_t j = pw_chk(p);
         return (tsyn[j >> 5] >> (j & 31)) & 1u;
@@ -203,7 +202,7 @@ __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan,
     if (t >= n_tasks) return;
     const uint2* pl = plan + lane;
     if (lane < DC) row[64 + lane] = 0.0f;
-    auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
+    auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
     uint2 wt = pl[t * 64];
     uint2 wn = pl[(t + NW) * 64];
     uint2 wnn = pl[(t + 2 * NW) * 64];
@@ -227,9 +226,9 @@ __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan,
         const uint32_t neg = ((tsyn[j >> 5] >> (j & 31)) & 1u) ^
                              (uint32_t)(DC <= 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^
                              (neg_t ? 1u : 0u);
-        // pv.y is never NaN (the sum enters through fminf), so clamp_msg of
-        // +-pv.y is +-min(pv.y, thr) (thr > 0: check_decode_params)
-        const float m = CLAMP ? __builtin_fminf(pv.y, thr) : pv.y;
+        // pv.y >= +0 is never NaN (the sum enters through fminf), so clamp_msg
+        // of +-pv.y is +-med3(pv.y, 0, thr) (thr > 0: check_decode_params)
+        const float m = CLAMP ? __builtin_amdgcn_fmed3f(pv.y, 0.0f, thr) : pv.y;
         ms.st(slot(wt), neg ? -m : m);
         row[lane] = pv.x;
         sgn_t = __ballot(xn < 0.0f);
@@ -344,8 +343,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
     // the row's DC entries past lane 63 are read (times 0) by segments ending
     // there: keep them finite (the prologue stages key words in this region)
     if (lane < DC) row[64 + lane] = 0.0;
-    // n_pad < 2^24 and rows < 32: a 24-bit multiply
-    auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
+    auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
     auto edge = [&](double xv, uint2 w) -> double {
         // phi(|b2c|) / ln 2 with the sign of b2c in the low word, NaN when
         // the sign is not certain (psi_of_exact); idle lanes (the dummy
@@ -353,7 +351,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         const f2 bv = qkds::unpack_iv(xv);
         const bool neg = bv.x < 0.0f;
         const bool ok = bv.x == bv.x;
-        bad |= !ok && pw_bit(w) != n_bits;
+        bad |= !ok && pw_slot(w) != n_bits;
         const f2 ph = ok ? (neg ? -bv.yx : bv) : f2{0.0f, 0.0f};
         row[lane] = qkds::pack_iv(ph);
         const uint64_t sgn = __ballot(neg);
@@ -438,7 +436,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
     bool bad = false;
     const uint2* pl = plan + lane;
     if (lane < DC) row[64 + lane] = 0.0;
-    auto slot = [&](uint2 p) -> uint32_t { return __umul24(pw_row(p), n_pad) + pw_bit(p); };
+    auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
     // |b2c| of an edge, its sign and whether the interval certifies it
     // (idle lanes, the dummy column, do not count)
     auto input = [&](double xv, uint2 w, bool& neg, f2& ab) -> bool {
@@ -446,7 +444,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         neg = bv.y < 0.0f;
         ab = neg ? -bv.yx : bv;
         const bool ok = (neg || bv.x > 0.0f) && ab.x > 1.0e-30f;
-        bad |= !ok && pw_bit(w) != n_bits;
+        bad |= !ok && pw_slot(w) != n_bits;
         return ok;
     };
     // (the plan has kPlanPadTasks idle tasks past n_tasks: loads ahead need no test)
@@ -852,23 +850,23 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     // (iteration 2 after the folded first one: the slots hold
                     // the phi bounds of exact b2c, psi_of_exact)
                     if (!folded && fold1 && it == 1) {
-                        spec_check_phase_psi<DC>(c.plan, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
+                        spec_check_phase_psi<DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
                                                    a.thr_up, rw, wave, lane);
                         __syncthreads();
                     } else if (!folded) {
-                        spec_check_phase_paired<DC>(c.plan, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
+                        spec_check_phase_paired<DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
                                                     a.thr_up, rw, wave, lane);
                         __syncthreads();
                     }
                 }
             } else if (!folded) {
                 if constexpr (RULE == kRuleSp32)
-                    sp32_check_phase<CLAMP, DC>(c.plan, tsyn, ms, row, wtab, n_tasks, n_pad, thr, wave, lane);
+                    sp32_check_phase<CLAMP, DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, thr, wave, lane);
                 else if (TABLES && it == 1 && tab2_on)
-                    split_check_phase<kSrcTable, CLAMP, DC, RULE>(c.plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
+                    split_check_phase<kSrcTable, CLAMP, DC, RULE>(c.plan_slot, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);
                 else
-                    split_check_phase<kSrcFirst, CLAMP, DC, RULE>(c.plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
+                    split_check_phase<kSrcFirst, CLAMP, DC, RULE>(c.plan_slot, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);
                 __syncthreads();
             }

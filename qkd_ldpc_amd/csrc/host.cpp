@@ -50,6 +50,8 @@ static void free_device(qkd_code* c) {
     c->d_pat_deg = nullptr;
     if (c->d_plan) (void)hipFree(c->d_plan);
     c->d_plan = nullptr;
+    if (c->d_plan_slot) (void)hipFree(c->d_plan_slot);
+    c->d_plan_slot = nullptr;
     if (c->d_jump) (void)hipFree(c->d_jump);
     c->d_jump = nullptr;
     c->d_chk_bits = nullptr;
@@ -217,6 +219,11 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     for (size_t k = 0; k < plan.word.size(); ++k) plan2[k] = make_uint2(plan.word[k], plan.seg[k]);
     QKD_HIP(hipMalloc(&c->d_plan, plan2.size() * sizeof(uint2)));
     QKD_HIP(hipMemcpy(c->d_plan, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    // the same plan slot-addressed (row * n_pad + bit; idle lanes: slot n)
+    for (size_t k = 0; k < plan.word.size(); ++k)
+        plan2[k].x = (plan.word[k] >> 24) * (uint32_t)c->n_pad + (plan.word[k] & qkdp::kPlanBitMask);
+    QKD_HIP(hipMalloc(&c->d_plan_slot, plan2.size() * sizeof(uint2)));
+    QKD_HIP(hipMemcpy(c->d_plan_slot, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
     // Key-generation jump-ahead: chunk = draws per lane, a multiple of 64 so
     // every lane's Alice bits fill whole words.
     const uint64_t draws = qkdr::trial_draws((uint32_t)n);

@@ -219,6 +219,8 @@ constexpr int kPlanGroup = 4;
 
 // ---- wave-plan words (qkd_plan.h) ------------------------------------------
 __device__ __forceinline__ uint32_t pw_bit(uint2 p) { return p.x & qkdp::kPlanBitMask; }
+// DeviceCode::plan_slot's first word: the edge's message slot
+__device__ __forceinline__ uint32_t pw_slot(uint2 p) { return p.x; }
 __device__ __forceinline__ uint32_t pw_row(uint2 p) { return p.x >> 24; }
 __device__ __forceinline__ uint32_t pw_chk(uint2 p) { return p.y & qkdp::kPlanChkMask; }
 __device__ __forceinline__ int pw_start(uint2 p) { return (int)((p.y >> 20) & 63u); }

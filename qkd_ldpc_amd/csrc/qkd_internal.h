@@ -75,6 +75,9 @@ struct DeviceCode {
     // bit's checks in ascending order (0 past its degree), 48-49 its degree,
     // 50-53 / 54-57 / 58-61 each check's degree - 1
     const uint64_t* bit_code;
+    // plan with the message slot row * n_pad + bit in place of {bit, row}
+    // (split kernels: their message store is slot-addressed)
+    const uint2* plan_slot;
 };
 
 }  // namespace qkd
@@ -129,6 +132,7 @@ struct qkd_code {
     uint8_t* d_bit_pos = nullptr;
     uint8_t* d_bit_deg = nullptr;
     uint2* d_plan = nullptr;
+    uint2* d_plan_slot = nullptr;
     int32_t n_pat = 0;                  // 0: too many degree patterns for the table
     std::vector<uint8_t> pat_deg;
     uint16_t* d_bit_pat = nullptr;
@@ -145,7 +149,7 @@ struct qkd_code {
     qkd::DeviceCode view() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
-                               n_pat, d_bit_pat, d_pat_deg, d_bit_code};
+                               n_pat, d_bit_pat, d_pat_deg, d_bit_code, d_plan_slot};
     }
 };
 
