@@ -339,6 +339,7 @@ def main():
             names = ["prologue", "check", "bit", "syndrome", "fetch_out", "check_first", "check_second"]
             tot = float(cyc.sum()) or 1.0
             out["phase_share"] = {n: float(v) / tot for n, v in zip(names, cyc)}
+            out["phase_cycles"] = {n: int(v) for n, v in zip(names, cyc)}
         if world == 1 and not args.no_e2e:
             out["end_to_end"] = measure_end_to_end(args, H, ws, seeds, F, Q, args.steps)
         if world == 1 and not args.no_variants:
