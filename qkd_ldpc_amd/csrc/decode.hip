@@ -1084,7 +1084,22 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
         // diagnostic: QKD_SPLIT_BUDGET lowers the LDS budget (fewer LDS slots)
         size_t budget = kLdsBytesMax;
         if (const char* b = getenv("QKD_SPLIT_BUDGET")) budget = std::min(budget, (size_t)atol(b));
-        const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, esz, budget);
+        // the speculative kernel (interval iterations, qkd_spec.h, exact
+        // replays in place) when it applies: QKD path with the folded first
+        // iteration, binary64 rule, clamped messages, bit degree <= kDvUnroll
+        // (the QKD path needs its folded first iteration; the LLR path starts from the LLRs)
+        const bool spec = rule == kRuleSp64 && a.spec_cap > 0 && a.clamp_on &&
+                          (mode == kModeLlr || a.first_table) && c->max_dv <= kDvUnroll && c->d_bit_code;
+        const bool ckpt = spec && mode == kModeKeys && a.ckpt_unsat > 0;
+        // its folded first iteration from a table (decode_split.hip fold_table_fill)
+        // (at most kFoldTabMaxEntries: the table's LDS comes off the message slots)
+        a.ftab_entries = (spec && !ckpt && mode == kModeKeys && a.tab2_entries &&
+                          c->n_pat * kFoldTabPat <= kFoldTabMaxEntries)
+                             ? c->n_pat * kFoldTabPat : 0;
+        // (QKD_FOLD_TABLE=0: the per-bit form; tests compare the two)
+        if (const char* e = getenv("QKD_FOLD_TABLE")) if (atoi(e) == 0) a.ftab_entries = 0;
+        const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, a.ftab_entries, esz,
+                         budget);
         // (the binary32 rule's kernel keeps every slot in LDS: SplitStore<float, true>)
         // (binary64: any share of the slots in LDS, the rest in the
         // workgroup's global region; long codes keep most of them there)
@@ -1100,7 +1115,14 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             a.code = c->view();
             a.c2b = ws->c2b;
             const size_t slots = (size_t)c->max_dv * c->n_pad;
-            a.c2b_stride = (slots - L.S + 31) & ~(size_t)31;      // elements of the message type
+            // elements of the message type, plus kC2bPad: the workgroups' regions
+            // start off a common alignment (measured: config 2 with the fold table
+            // has a region of 13184 slots, 4 % slower than 13248;
+            // QKD_C2B_PAD overrides the pad)
+            size_t pad = kC2bPad;
+            if (const char* e = getenv("QKD_C2B_PAD")) pad = (size_t)atol(e);
+            pad = std::min(pad, (size_t)c->n_pad);   // the region stays inside ws_reserve_decode's
+            a.c2b_stride = ((slots - L.S + 31) & ~(size_t)31) + pad;
             a.lds_budget = (uint32_t)budget;
             a.counter = ws->counter;
             QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));     // [0] frame queue, [1] replays
@@ -1117,15 +1139,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 a.zout = ws->zout;
                 QKD_HIP(launch_frame_syn(a, stream));
             }
-            // the speculative kernel (interval iterations, qkd_spec.h, exact
-            // replays in place) when it applies: QKD path with the folded first
-            // iteration, binary64 rule, clamped messages, bit degree <= kDvUnroll
-            // (the QKD path needs its folded first iteration; the LLR path starts from the LLRs)
-            const bool spec = rule == kRuleSp64 && a.spec_cap > 0 && a.clamp_on &&
-                              (mode == kModeLlr || a.first_table) && c->max_dv <= kDvUnroll && c->d_bit_code;
             if (spec) {
                 int xdc = 0, sgrid = 0;
-                const bool ckpt = mode == kModeKeys && a.ckpt_unsat > 0;
                 DecodeFn xfn = pick_split_spec(mode, c->max_dc, ckpt, &xdc);
                 s = decode_grid(c, xfn, L.bytes, &sgrid);
                 if (s != QKD_OK) return s;

@@ -505,6 +505,47 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
     if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
 }
 
+// The folded first iteration as a table (speculative kernel, QKD path): its
+// messages are +-C_d (first_check_phase), so a bit's exact total and the psi
+// bounds of its b2c (spec_bit_phase, FOLD) depend only on its degree pattern
+// p, Bob's bit and the signs of its three messages: entry
+//   ftab[(p * 16 + code) * 4 + k],  code = bob | sign_k << (1 + k)
+// holds psi_of_exact(clamp(total - c_k)) for row k < 3 (packed) and, at k = 3,
+// whether total <= 0 (the hard decision), each computed with the binary64
+// operations of the per-bit form in the same order (tests/test_spec.py runs
+// both forms).
+__device__ void fold_table_fill(const DeviceCode& c, const double* ctab, double log_p, double thr, double* ftab,
+                                int entries) {
+    static_assert(kFoldTabPat == 64, "16 codes x 4 entries");
+    for (int e = threadIdx.x; e < entries; e += kDecodeBlock) {
+        const int p = e / kFoldTabPat;
+        const uint32_t code = ((uint32_t)e >> 2) & 15u;
+        const int k = e & 3;
+        const uint8_t* degs = c.pat_deg + p * c.max_dv;
+        double acc = (code & 1u) ? -log_p : log_p;
+        double cv[kDvUnroll];
+        int dv = 0;
+#pragma unroll
+        for (int m = 0; m < kDvUnroll; ++m) {
+            const int d = m < c.max_dv ? (int)degs[m] : 0;
+            if (d != 0 && dv == m) dv = m + 1;
+            const double cm = ctab[d];
+            cv[m] = ((code >> (1 + m)) & 1u) ? -cm : cm;
+        }
+#pragma unroll
+        for (int m = 0; m < kDvUnroll; ++m) acc = m < dv ? acc + cv[m] : acc;
+        double v = 0.0;
+        if (k == kDvUnroll) {
+            v = __builtin_bit_cast(double, (unsigned long long)(acc <= 0 ? 1 : 0));
+        } else if (k < dv) {
+            const double ck = k == 0 ? cv[0] : (k == 1 ? cv[1] : cv[2]);
+            v = qkds::pack_iv(qkds::psi_of_exact(clamp_msg(acc - ck, thr)));
+        }
+        ftab[e] = v;
+    }
+    __syncthreads();
+}
+
 // Bit phase on intervals. FOLD (the first iteration): the messages are the
 // exact +-C_d of first_check_phase, so the totals are computed in binary64
 // exactly as the exact path does and the b2c are stored as enclosing
@@ -525,7 +566,8 @@ constexpr int kIvChunk = QKD_IV_CHUNK;       // rounds per load batch
 // guards every row by the bit's degree.
 template <bool FOLD, int MODE, bool DV3>
 __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const DecodeArgs& a, const SplitStore<double>& ms,
-                                               const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
+                                               const uint32_t* qsyn, const double* ctab, const double* ftab,
+                                               uint32_t* xsyn,
                                                uint32_t* xunc, uint64_t* zw, uint64_t bobmask, bool keep,
                                                uint32_t f, int tid, int wave, int lane) {
     using qkds::f2;
@@ -536,11 +578,13 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
     for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kIvChunk) {
         double v[kIvChunk][kDvUnroll];
         uint64_t bc[kIvChunk];                 // the bits' packed words (DeviceCode::bit_code)
+        uint32_t pat[kIvChunk];                // FOLD with ftab: the bits' degree patterns
 #pragma unroll
         for (int u = 0; u < kIvChunk; ++u) {
             const int i = tid + (r0 + u) * kDecodeBlock;
             const bool ok = i < c.n;
             bc[u] = ok ? c.bit_code[i] : 0;
+            pat[u] = (FOLD && ftab && ok) ? (uint32_t)c.bit_pat[i] : 0u;
             const uint32_t iw = (uint32_t)((r0 + u) * kDecodeBlock + wave * 64);
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k)
@@ -562,7 +606,21 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             const uint32_t bob = (uint32_t)(bobmask >> r) & 1u;
             bool z, unc = false;
             f2 bo[kDvUnroll];
-            if (FOLD) {
+            if (FOLD && ftab) {
+                // the same from the table (fold_table_fill): the code of Bob's
+                // bit and the message signs picks the bit's psi bounds and decision
+                const uint32_t sgi = bob ^ lsign;
+                uint32_t code = bob;
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k) {
+                    const int j = jc[k];
+                    code |= (((qsyn[j >> 5] >> (j & 31)) & 1u) ^ sgi) << (1 + k);
+                }
+                const double* e = ftab + (pat[u] * 16u + code) * 4u;
+#pragma unroll
+                for (int k = 0; k < kDvUnroll; ++k) bo[k] = qkds::unpack_iv(e[k]);
+                z = ok && __builtin_bit_cast(unsigned long long, e[kDvUnroll]) != 0ull;
+            } else if (FOLD) {
                 // the exact first iteration (fold_first_message, then :256-267, :303-316)
                 const uint32_t sgi = bob ^ lsign;
                 double acc = bob ? -llr_p : llr_p;
@@ -667,7 +725,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
-    const SplitLds L(c.n_pad, (c.n + 63) / 64, c.m, c.max_dv, DC, a.tab2_entries, (int)sizeof(T), a.lds_budget);
+    const SplitLds L(c.n_pad, (c.n + 63) / 64, c.m, c.max_dv, DC, a.tab2_entries, a.ftab_entries, (int)sizeof(T),
+                     a.lds_budget);
     const int m_words = decode_m_words(c.m);
     uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
@@ -729,6 +788,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     if (tab2_on) {
         __syncthreads();
         second_table_fill<CLAMP>(c, ctab, a.log_p, a.thr, tab2, a.tab2_entries);
+    }
+    double* ftab = nullptr;
+    if constexpr (SPEC == 1) {
+        if (fold1 && a.ftab_entries) {
+            ftab = reinterpret_cast<double*>(smem + L.ftab);
+            __syncthreads();
+            fold_table_fill(c, ctab, a.log_p, a.thr, ftab, a.ftab_entries);
+        }
     }
     PhaseClock pc(a.phase);
 
@@ -880,17 +947,17 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                 if constexpr (SPEC) {
                     if (dv3) {
                         if (folded)
-                            spec_bit_phase<true, MODE, true>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
+                            spec_bit_phase<true, MODE, true>(c, a, ms, qsyn, ctab, ftab, xsyn, xunc, zw, bobmask, keep,
                                                              f, tid, wave, lane);
                         else
-                            spec_bit_phase<false, MODE, true>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
+                            spec_bit_phase<false, MODE, true>(c, a, ms, qsyn, ctab, ftab, xsyn, xunc, zw, bobmask, keep,
                                                               f, tid, wave, lane);
                     } else {
                         if (folded)
-                            spec_bit_phase<true, MODE, false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
+                            spec_bit_phase<true, MODE, false>(c, a, ms, qsyn, ctab, ftab, xsyn, xunc, zw, bobmask, keep,
                                                               f, tid, wave, lane);
                         else
-                            spec_bit_phase<false, MODE, false>(c, a, ms, qsyn, ctab, xsyn, xunc, zw, bobmask, keep,
+                            spec_bit_phase<false, MODE, false>(c, a, ms, qsyn, ctab, ftab, xsyn, xunc, zw, bobmask, keep,
                                                                f, tid, wave, lane);
                     }
                 }

@@ -73,6 +73,10 @@ struct DecodeArgs {
     // Second-iteration tanh table (kModeKeys, needs first_table): entries,
     // 0 when off (see second_table_fill).
     int tab2_entries;
+    // speculative kernel, QKD path: entries of the folded first iteration's
+    // table (kFoldTabPat per degree pattern, decode_split.hip fold_table_fill),
+    // 0 when off
+    int ftab_entries;
     // outputs
     uint8_t* bits_out;
     uint32_t* iters;
@@ -205,6 +209,9 @@ struct DecodeLds {
 // Bit phase: message rows per bit loaded ahead of the ordered sum, and rounds
 // (bits tid + r*kDecodeBlock) per load batch.
 constexpr int kDvUnroll = 3;
+// fold table entries per degree pattern: 2^(1 + kDvUnroll) sign codes x
+// (kDvUnroll psi bounds + the hard decision)
+constexpr int kFoldTabPat = (2 << kDvUnroll) * (kDvUnroll + 1);
 constexpr int kBitChunk = 5;
 #ifndef QKD_SPEC_EXACT_CHUNK
 #define QKD_SPEC_EXACT_CHUNK 2
@@ -462,6 +469,8 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 //                                (prologue: the frame's Alice + Bob words)
 //   ctab  [kFirstTableDeg + 1]   first-iteration message magnitudes by degree
 //   tab2  [tab2_entries]         second-iteration tanh table
+//   ftab  [ftab_entries]         speculative kernel: the folded first
+//                                iteration's psi bounds and hard decisions
 //   ctl   [8]                    [1] next frame, [4..5] round flags (decode_split.hip)
 //   wtab  [dc][dc][dc] float     extrinsic-sum weights by (degree, position, k) (dc <= 8)
 //   msg   [S + 64] T             message slots 0 .. S-1 (slots S .. max_dv*n_pad-1
@@ -475,10 +484,10 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 __host__ __device__ inline int seg_weight_entries(int dc) { return dc <= 8 ? dc * dc * dc : 0; }
 
 struct SplitLds {
-    size_t tsyn, xsyn, qsyn, xunc, zw, tval, ctab, tab2, ctl, wtab, msg, bytes;
+    size_t tsyn, xsyn, qsyn, xunc, zw, tval, ctab, tab2, ftab, ctl, wtab, msg, bytes;
     uint32_t S;
-    __host__ __device__ SplitLds(int n_pad, int n_words, int m, int max_dv, int dc, int tab2_entries, int esz,
-                                 size_t budget) {
+    __host__ __device__ SplitLds(int n_pad, int n_words, int m, int max_dv, int dc, int tab2_entries,
+                                 int ftab_entries, int esz, size_t budget) {
         const int m_words = decode_m_words(m);
         tsyn = 0;
         xsyn = tsyn + (size_t)m_words * 4;
@@ -490,7 +499,8 @@ struct SplitLds {
         const size_t stage = (size_t)n_words * 16;
         ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
-        ctl = (tab2 + (size_t)tab2_entries * 8 + 15) & ~(size_t)15;
+        ftab = (tab2 + (size_t)tab2_entries * 8 + 15) & ~(size_t)15;
+        ctl = (ftab + (size_t)ftab_entries * 8 + 15) & ~(size_t)15;
         wtab = ctl + 32;
         msg = (wtab + (size_t)seg_weight_entries(dc) * 4 + 15) & ~(size_t)15;
         const size_t slots = (size_t)max_dv * n_pad;

@@ -19,6 +19,8 @@ constexpr int kDecodeBlock = 1024;
 // max_dv <= kTab2MaxDv and n_pat * entries <= kTab2MaxEntries.
 constexpr int kTab2MaxDv = 3;   // <= the bit phase's unrolled rows (decode.hip kDvUnroll)
 constexpr int kTab2MaxEntries = 2048;
+constexpr int kFoldTabMaxEntries = 1024;   // speculative fold table (decode_split.hip), 8 B each
+constexpr size_t kC2bPad = 64;             // split kernels: slots added to each workgroup's global region
 __host__ __device__ inline int tab2_stride(int max_dv) { return (1 << (1 + max_dv)) * max_dv; }
 
 // Largest check degree: one check's edges fit one wavefront (qkd_plan.h).

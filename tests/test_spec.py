@@ -394,6 +394,28 @@ def test_spec_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q):
               f"mean it {ex.iterations.double().mean().item():.3f}")
 
 
+@pytest.mark.parametrize("q", [0.02, 0.04, 0.06])
+def test_fold_table_equals_per_bit_form(Q, H, fresh_seeds, monkeypatch, q):
+    """The speculative kernel's folded first iteration from its per-pattern table
+    (fold_table_fill) against the per-bit form (QKD_FOLD_TABLE=0): the same psi
+    bounds give the same certified rounds, so outputs AND the count of frames the
+    intervals could not certify agree."""
+    seeds = fresh_seeds[:20_000]
+    out = {}
+    for tab in ("0", "1"):
+        monkeypatch.setenv("QKD_FOLD_TABLE", tab)
+        ws = Q.Workspace(H)
+        alice, bob, _ = Q.keygen(H, seeds, q, 0, workspace=ws)
+        Q.spec_replays(ws, reset=True)
+        r = Q.qkd_ldpc(H, alice, bob, q, 50, 100.0, True, want_bits=True, workspace=ws)
+        torch.cuda.synchronize()
+        out[tab] = (r, Q.spec_replays(ws))
+    (a, na), (b, nb) = out["0"], out["1"]
+    assert torch.equal(a.iterations, b.iterations) and torch.equal(a.bits, b.bits)
+    assert torch.equal(a.keys_match, b.keys_match) and torch.equal(a.syndromes_match, b.syndromes_match)
+    assert na == nb, (q, na, nb)
+
+
 @pytest.mark.parametrize("q", [0.02, 0.05])
 def test_spec_llr_path_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q):
     """The LLR entry (sum_product_decoding) on 100,000 fresh frames with LLRs that are
