@@ -48,7 +48,9 @@ VARIANTS = {"sp_f64": {"variant": "sp_f64"}, "sp_f32": {"variant": "sp_f32"}, "m
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under torchrun, else 1); without "
+                         "torchrun, N > 1 starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames", type=int, default=4096)
@@ -66,6 +68,8 @@ def parse():
                     help="decoder rule of the headline line (sp_f64 = the reference's)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the side measurement of the binary32 variants")
+    ap.add_argument("--no-sweeps", action="store_true",
+                    help="skip the config-3 QBER sweep and the config-4 rank-share lines")
     return ap.parse_args()
 
 
@@ -94,30 +98,73 @@ def pmc_record(variant):
         return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
-def roofline_block(variant, alg_bytes, kernel_s, kernel_name):
-    """roofline: algorithmic bytes / the launch's HIP-event time
-    against the 8 TB/s HBM peak (nominal: the formulation here moves fewer bytes),
-    plus what the PMC record measured for the same kernel."""
+def rocprof_warm_ms(kernel):
+    """Warm average duration of `kernel` in the newest committed rocprofv3
+    --kernel-trace summary (profiles/r*_kernel_summary.json, tools/prof_summary.py)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_summary.json")))
+    for path in reversed(files):
+        with open(path) as f:
+            for r in json.load(f)["kernels"]:
+                if r["kernel"] == kernel:
+                    return r["warm_avg_ms"], os.path.relpath(path, ROOT)
+    return None, None
+
+
+def roofline_block(variant, alg_bytes, kernel_s, call_s, kernel_name):
+    """roofline (the contract's block): algorithmic bytes per launch
+    / the DECODE KERNEL's average duration, measured live with HIP events recorded
+    around its launch on its own stream (qkd_debug_decoder_timing), against the 8 TB/s
+    HBM peak. `frac` is nominal: this formulation moves far fewer bytes than the
+    reference's two-array one. Alongside:
+      frac_call     the same bytes over the whole library call (pack, frame syndromes,
+                    decoder, key compare: HIP events around the call);
+      frac_kernel   the same bytes over the committed rocprof warm average of the kernel;
+      binding       what the PMC record of the kernel measured: DRAM bytes per launch
+                    as a fraction of the HBM peak over this kernel time, and the VALU
+                    active fraction (SQ_ACTIVE_INST_VALU x 4 quad-cycles / cycles x SIMDs);
+                    `limiter` names the larger."""
     achieved = alg_bytes / kernel_s / 1e9
     rec, src = pmc_record(variant)
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
-           "nominal": True, "kernel": kernel_name, "kernel_ms": kernel_s * 1e3,
+           "nominal": True, "kernel": kernel_name, "kernel_ms": kernel_s * 1e3, "call_ms": call_s * 1e3,
+           "frac_call": alg_bytes / call_s / 1e9 / HBM_PEAK_GBS,
            "algorithmic_bytes_per_launch": alg_bytes, "traffic_source": src}
     if rec:
-        out["dram_gbs_measured"] = rec["hbm_bytes_per_launch"] / kernel_s / 1e9
-        if "valu" in rec:
-            out["valu"] = rec["valu"]
         out["pmc_kernel"] = rec.get("kernel")
+        warm, wsrc = rocprof_warm_ms(rec.get("kernel"))
+        if warm:
+            out["frac_kernel"] = alg_bytes / (warm / 1e3) / 1e9 / HBM_PEAK_GBS
+            out["rocprof_warm_ms"] = warm
+            out["rocprof_source"] = wsrc
+        v = rec.get("valu", {})
+        dram = rec["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS
+        act = v.get("valu_active_util_x4")
+        out["binding"] = {"dram_frac": dram, "valu_active_frac": act,
+                          "valu_insts_per_launch": v.get("valu_insts_per_launch"),
+                          "wait_frac": v.get("wait_frac"), "lds_conflict_frac": v.get("lds_conflict_frac"),
+                          "effective_clock_ghz": v.get("effective_clock_ghz"),
+                          "limiter": "valu" if (act or 0) > dram else "hbm"}
     return out
 
 
-def measure_variants(args, step, stream, counters, iters, Q, F, q, steps=5):
+def decoder_ms(L, ws, start):
+    """qkd_debug_decoder_timing: start, or collect the average decoder-kernel ms."""
+    import ctypes as C
+    from qkd_ldpc_amd import _native as N
+    tot, n = C.c_double(0), C.c_uint64(0)
+    N.check(L.qkd_debug_decoder_timing(ws.handle, 1 if start else 0, C.byref(tot), C.byref(n)))
+    return tot.value / n.value if n.value else None
+
+
+def measure_variants(args, step, stream, counters, iters, Q, F, q, L, ws, steps=5):
     """Side measurement on the same resident keys: the build-defined binary32
     variants (QKD_VARIANT_SP_F32, QKD_VARIANT_MINSUM plain and self-corrected;
     SURVEY.md §8(d) config 5),
-    timed like the headline (wall clock over `steps` steps, HIP events for the
-    decode kernel). Their FER is a property of the decoder, not a parity claim."""
+    timed like the headline (wall clock over `steps` steps, HIP events around the
+    decode kernel and around the call). Their FER is a property of the decoder, not a
+    parity claim. Their roofline block's `bound` is what their PMC record shows (their
+    message stores live in LDS: they are not HBM-bound)."""
     import torch
     out = {}
     for v in VARIANTS:
@@ -127,18 +174,23 @@ def measure_variants(args, step, stream, counters, iters, Q, F, q, steps=5):
         torch.cuda.synchronize()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(steps)]
+        decoder_ms(L, ws, True)
         t0 = time.perf_counter()
         for k in range(steps):
             step(evs[k], variant=v)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        kms = decoder_ms(L, ws, False)
         st = Q.counters_to_stats(Q.read_counters(counters), F, args.max_iters, q)
-        kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        cms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
         b_iter = B_ITER if v == "sp_f64" else B_ITER32
         alg = int(iters.cpu().numpy().astype(np.int64).sum()) * b_iter + F * B_FRAME
-        out[v] = {"value": F * N_BITS * steps / el, "unit": "bit/s", "kernel_ms": kms,
-                  "fer": st["fer"], "mean_iterations": st["iterations_successful_sp_mean"],
-                  "roofline": roofline_block(v, alg, kms / 1e3, f"qkd_qkd_ldpc_batch, variant {v}")}
+        rb = roofline_block(v, alg, kms / 1e3, cms / 1e3, f"decoder kernel of qkd_qkd_ldpc_batch, variant {v}")
+        if "binding" in rb:
+            rb["bound"] = rb["binding"]["limiter"]
+            rb["nominal_hbm_frac"] = rb["frac"]
+        out[v] = {"value": F * N_BITS * steps / el, "unit": "bit/s", "kernel_ms": kms, "call_ms": cms,
+                  "fer": st["fer"], "mean_iterations": st["iterations_successful_sp_mean"], "roofline": rb}
     return out
 
 
@@ -161,6 +213,69 @@ def measure_end_to_end(args, H, ws, seeds, F, Q, steps):
             "what": "qkd_trials_batch: keygen_fast_kernel + frame_syn + decoder + key_match + counters"}
 
 
+def config3_sweep(args, H, Q, dev):
+    """BASELINE configs[2]: the FER curve, QBER 0.01 ... 0.08 (qber_range(0.01, 0.09, 0.01)),
+    10,000 trials per point, point s seeding frame k with seeds[k] + s
+    (simulation.cpp:231-312), one qkd_trials_batch per point (device keygen included,
+    as run_trial times it) on a fresh workspace, in the reference's point order. The
+    reference's own table (measured on 8 Xeon threads in 145.5 s) sits
+    beside each point; with the bit-exact decoder FER and mean iterations must equal it
+    to its printed digits."""
+    import torch
+    with open(os.path.join(ROOT, "tests", "golden", "reference_probe.json")) as f:
+        ref = json.load(f)["config3"]
+    trials = ref["trials"]
+    grid = Q.qber_range(ref["qber_begin"], ref["qber_end"], ref["qber_step"])
+    seeds = torch.from_numpy(Q.make_seeds(args.seed, trials).view(np.int64)).to(dev)
+    ws = Q.Workspace(H)
+    Q.run_trials(H, seeds[:256], grid[0], 0, args.max_iters, args.threshold, True, workspace=ws)   # warm
+    torch.cuda.synchronize()
+    points, total = [], 0.0
+    for s_, qn in enumerate(grid):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = Q.run_trials(H, seeds, qn, s_, args.max_iters, args.threshold, True, workspace=ws)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        total += dt
+        st = Q.counters_to_stats(Q.read_counters(r.counters), trials, args.max_iters,
+                                 float(r.exact_qber[0].item()))
+        rp = ref["points"][s_]
+        points.append({"qber_nominal": qn, "qber_actual": float(r.exact_qber[0].item()), "ms": dt * 1e3, "fer": st["fer"],
+                       "mean_iterations": st["iterations_successful_sp_mean"],
+                       "sum_iterations": st["sum_iters_sp"],
+                       "reference": {"qber_actual": rp["qber_actual"], "fer": rp["fer"], "mean_it": rp["mean_it"]},
+                       "matches_reference": bool(abs(st["fer"] - rp["fer"]) < 1e-12 and
+                                                 abs(st["iterations_successful_sp_mean"] - rp["mean_it"]) <= 5e-4)})
+    ws.close()
+    return {"what": "configs[2]: 8 QBER points x 10,000 trials, qkd_trials_batch per point (keygen + decode + "
+                    "counters), fresh workspace, ascending points", "total_s": total,
+            "reference_total_s_8_xeon_threads": 145.5, "points": points}
+
+
+def config4_rank_share(args, H, Q, dev, frames=125_000):
+    """BASELINE configs[3] on one GPU: one rank's share of the 1M-frame config-2 run over
+    8 GPUs, 125,000 frames (seeds[0:125000]) in ONE qkd_trials_batch (device keygen
+    included), timed warm."""
+    import torch
+    seeds = torch.from_numpy(Q.make_seeds(args.seed, frames).view(np.int64)).to(dev)
+    ws = Q.Workspace(H)
+    r = Q.run_trials(H, seeds, args.qber, 0, args.max_iters, args.threshold, True, workspace=ws)
+    torch.cuda.synchronize()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        Q.run_trials(H, seeds, args.qber, 0, args.max_iters, args.threshold, True, workspace=ws, out=r)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    st = Q.counters_to_stats(Q.read_counters(r.counters), frames, args.max_iters, float(r.exact_qber[0].item()))
+    ws.close()
+    return {"what": "configs[3] rank share: 125,000 config-2 frames in one qkd_trials_batch (keygen + decode + "
+                    "counters), warm, mean of 3", "frames": frames, "ms": dt * 1e3,
+            "value": frames * N_BITS / dt, "unit": "bit/s", "fer": st["fer"],
+            "sum_iterations": st["sum_iters_sp"], "mean_iterations": st["iterations_successful_sp_mean"]}
+
+
 def cpu_calibration():
     p = os.path.join(ROOT, "profiles", "cpu_calibration.json")
     if not os.path.exists(p):
@@ -175,7 +290,15 @@ def cpu_calibration():
 
 def cpu_baseline(args, g):
     """The oracle (CPU restatement of the reference, glibc libm, -O3) on a bounded
-    sample of the same workload, one frame per task on `threads` host threads."""
+    sample of the same workload, one frame per task on `threads` host threads.
+
+    Core count: the GPU box gives each GPU a 16-CPU host share (worker pools are
+    sized to it there: OMP_NUM_THREADS and the pool's rules), while
+    os.sched_getaffinity shows the whole machine. The measured figure uses that
+    share (`cores`); `all_cores_estimate` scales it linearly to every affinity CPU
+    (the reference's frames are independent tasks on a thread pool,
+    simulation.cpp:230-250, so its throughput scales with cores until memory
+    bandwidth binds: an upper estimate, not a measurement)."""
     from oracle import oracle as O
     O.build()
     code = O.Code.from_lists(g)
@@ -190,10 +313,12 @@ def cpu_baseline(args, g):
     r = code.trials(args.qber, seeds, 0, args.max_iters, args.threshold, True, threads=threads)
     dt = time.perf_counter() - t0
     cal = cpu_calibration()
+    value = frames * N_BITS / dt
+    ratio = cal["oracle_over_reference_time"] if cal else None
     return {
-        "value": frames * N_BITS / dt,
+        "value": value,
         "unit": "bit/s",
-        "reference_equivalent_value": frames * N_BITS / dt * cal["oracle_over_reference_time"] if cal else None,
+        "reference_equivalent_value": value * ratio if cal else None,
         "cores": threads,
         "kind": "port",
         "sample": f"{frames} frames of the same config (seeds 777[0:{frames}]), "
@@ -201,6 +326,10 @@ def cpu_baseline(args, g):
                   f"{float(np.mean(r['iters'])):.4f}",
         "host_cpus_visible": os.cpu_count(),
         "host_cpus_affinity": avail,
+        "all_cores_estimate": {"cores": avail, "value": value * avail / threads,
+                               "reference_equivalent_value": value * avail / threads * ratio if cal else None,
+                               "how": f"linear scaling of the {threads}-thread measurement to {avail} CPUs "
+                                      "(not run: the box's worker-pool share is 16 CPUs per GPU)"},
         "cores_note": "one thread per core of this GPU's host CPU share (16 per GPU on the "
                       "MI355X pool; os.cpu_count() shows the whole machine)",
         "calibration": cal,
@@ -209,23 +338,22 @@ def cpu_baseline(args, g):
 
 def main():
     args = parse()
+    from qkd_ldpc_amd.dist import init_rank, rank_env, spawn_ranks
+
+    env = rank_env()
+    if env is None and (args.gpus or 1) > 1:
+        # one process per GPU, started here (no HIP call in this parent process)
+        sys.exit(spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    rank, world, local = env or (0, 1, 0)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with the launcher's WORLD_SIZE {world}")
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # one process per GPU over RCCL ("nccl"); QKD_DIST_BACKEND=gloo with more
+    if env is not None:
+        # RCCL ("nccl") with one device per rank; QKD_DIST_BACKEND=gloo with more
         # ranks than GPUs rehearses the multi-rank path on one device (tests)
-        backend = os.environ.get("QKD_DIST_BACKEND", "nccl")
-        if backend != "nccl":
-            local %= torch.cuda.device_count()
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        init_rank(world, local)
     import qkd_ldpc_amd as Q
 
     H, g = load_code(torch.cuda.current_device())
@@ -271,6 +399,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    decoder_ms(L, ws, True)      # HIP events around each decoder launch, on its stream
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
@@ -278,6 +407,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    dec_ms = decoder_ms(L, ws, False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -292,7 +422,8 @@ def main():
     sum_it_local = int(it_np.astype(np.int64).sum())
     b_iter = B_ITER if args.variant == "sp_f64" else B_ITER32
     alg_bytes = sum_it_local * b_iter + F * B_FRAME
-    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    avg_call_s = float(np.mean(kernel_ms)) / 1e3
+    avg_kernel_s = dec_ms / 1e3
     replays = Q.spec_replays(ws, reset=True)
 
     stats = Q.counters_to_stats(c, frames_total, args.max_iters, q)
@@ -323,9 +454,9 @@ def main():
             "mean_iterations": stats["iterations_successful_sp_mean"],
             "sum_iterations": stats["sum_iters_sp"],
             "roofline": roofline_block(
-                args.variant, alg_bytes, avg_kernel_s,
-                "qkd_qkd_ldpc_batch = frame_syn_kernel + decode_split_kernel + key_match_kernel "
-                "(+ pack of Alice/Bob), HIP events on its stream"),
+                args.variant, alg_bytes, avg_kernel_s, avg_call_s,
+                "decode_split_kernel (HIP events around its launch on its stream); call = "
+                "qkd_qkd_ldpc_batch: pack + frame_syn_kernel + decoder + key_match_kernel"),
             "speculation": {
                 "replayed_frames": replays,
                 "frames": F * (args.steps + args.warmup),
@@ -343,11 +474,14 @@ def main():
         if world == 1 and not args.no_e2e:
             out["end_to_end"] = measure_end_to_end(args, H, ws, seeds, F, Q, args.steps)
         if world == 1 and not args.no_variants:
-            out["variants"] = measure_variants(args, step, stream, counters, iters, Q, F, q)
+            out["variants"] = measure_variants(args, step, stream, counters, iters, Q, F, q, L, ws)
+        if world == 1 and not args.no_sweeps:
+            out["config3_sweep"] = config3_sweep(args, H, Q, dev)
+            out["config4_rank_share"] = config4_rank_share(args, H, Q, dev)
         if world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
             out["cpu_baseline"] = cpu_baseline(args, g)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -71,21 +71,34 @@ struct CodeKey {
 // simulation.cpp:108,134), so a different matrix can reappear at a reused row-pointer
 // address with the same n and m: every hit re-compares the rows (O(E) int compares,
 // microseconds against a device call) and a mismatch rebuilds the entry.
+//
+// Lifetime: the cache and every call in flight hold the code by shared_ptr, and
+// each cache entry carries a generation number. Per-thread workspaces are keyed by
+// that number (never by the qkd_code address, which a new code may reuse), and a
+// thread drops its workspaces of superseded generations on its next call; the
+// superseded code object is destroyed once the last of those references goes.
+struct CodeRef {
+    std::shared_ptr<qkd_code> code;
+    uint64_t gen = 0;
+    qkd_code* get() const { return code.get(); }
+};
+
 struct CachedCode {
-    qkd_code* code = nullptr;
+    CodeRef ref;
     std::vector<int32_t> ptr, idx;
 };
 
 std::mutex g_codes_mu;
+// (never destroyed: no device call runs during static destruction at exit)
 std::map<CodeKey, CachedCode>& codes() {
-    static std::map<CodeKey, CachedCode> m;
-    return m;
+    static auto* m = new std::map<CodeKey, CachedCode>();
+    return *m;
 }
-// Superseded code objects stay alive: per-thread workspaces are keyed by the
-// qkd_code pointer, so a retired object must never be freed and its address reused.
-std::vector<qkd_code*>& retired_codes() {
-    static std::vector<qkd_code*> v;
-    return v;
+uint64_t g_next_gen = 1;
+// generations still in the cache (read by ThreadCtx::workspace under g_codes_mu)
+std::map<uint64_t, bool>& live_gens() {
+    static auto* m = new std::map<uint64_t, bool>();
+    return *m;
 }
 
 // Row length the reference loops over: max weights for the regular twins
@@ -104,15 +117,15 @@ bool same_rows(const H_matrix& H, const CachedCode& c) {
     return true;
 }
 
-qkd_code* code_for(const H_matrix& H) {
+CodeRef code_for(const H_matrix& H) {
     if (!H.check_nodes || H.num_bit_nodes == 0 || H.num_check_nodes == 0)
         throw std::runtime_error("H_matrix is empty");
     const CodeKey key{H.check_nodes, H.num_bit_nodes, H.num_check_nodes};
     std::lock_guard<std::mutex> lk(g_codes_mu);
     auto it = codes().find(key);
     if (it != codes().end()) {
-        if (same_rows(H, it->second)) return it->second.code;
-        retired_codes().push_back(it->second.code);
+        if (same_rows(H, it->second)) return it->second.ref;
+        live_gens().erase(it->second.ref.gen);      // superseded: freed with its last reference
         codes().erase(it);
     }
     CachedCode cc;
@@ -122,12 +135,15 @@ qkd_code* code_for(const H_matrix& H) {
         cc.ptr[j + 1] = (int32_t)cc.idx.size();
     }
     qkd_status st = QKD_OK;
-    cc.code = qkd_code_create((int32_t)H.num_bit_nodes, (int32_t)H.num_check_nodes, cc.ptr.data(), cc.idx.data(),
-                              device_index(), &st);
-    if (!cc.code) fail("qkd_code_create");
-    qkd_code* c = cc.code;
+    qkd_code* raw = qkd_code_create((int32_t)H.num_bit_nodes, (int32_t)H.num_check_nodes, cc.ptr.data(),
+                                    cc.idx.data(), device_index(), &st);
+    if (!raw) fail("qkd_code_create");
+    cc.ref.code = std::shared_ptr<qkd_code>(raw, qkd_code_destroy);
+    cc.ref.gen = g_next_gen++;
+    live_gens()[cc.ref.gen] = true;
+    CodeRef r = cc.ref;
     codes().emplace(key, std::move(cc));
-    return c;
+    return r;
 }
 
 // ---- per-thread device context --------------------------------------------
@@ -152,7 +168,12 @@ struct DevBuf {
 
 struct ThreadCtx {
     hipStream_t stream = nullptr;
-    std::map<const qkd_code*, qkd_workspace*> ws;
+    // workspaces by code generation (CodeRef), each holding its code alive
+    struct WsEntry {
+        std::shared_ptr<qkd_code> code;
+        qkd_workspace* ws;
+    };
+    std::map<uint64_t, WsEntry> ws;
     DevBuf<double> llr, q;
     DevBuf<uint8_t> syn, bits, alice, bob, sp, ko;
     DevBuf<uint32_t> iters;
@@ -162,16 +183,29 @@ struct ThreadCtx {
         hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
     }
     ~ThreadCtx() {
-        for (auto& kv : ws) qkd_workspace_destroy(kv.second);
+        for (auto& kv : ws) qkd_workspace_destroy(kv.second.ws);
         if (stream) (void)hipStreamDestroy(stream);
     }
-    qkd_workspace* workspace(const qkd_code* c) {
-        auto it = ws.find(c);
-        if (it != ws.end()) return it->second;
+    qkd_workspace* workspace(const CodeRef& c) {
+        {
+            // drop the workspaces of superseded generations (and so this
+            // thread's references to their codes)
+            std::lock_guard<std::mutex> lk(g_codes_mu);
+            for (auto it = ws.begin(); it != ws.end();) {
+                if (live_gens().count(it->first)) {
+                    ++it;
+                    continue;
+                }
+                qkd_workspace_destroy(it->second.ws);
+                it = ws.erase(it);
+            }
+        }
+        auto it = ws.find(c.gen);
+        if (it != ws.end()) return it->second.ws;
         qkd_status st = QKD_OK;
-        qkd_workspace* w = qkd_workspace_create(c, &st);
+        qkd_workspace* w = qkd_workspace_create(c.get(), &st);
         if (!w) fail("qkd_workspace_create");
-        ws.emplace(c, w);
+        ws.emplace(c.gen, WsEntry{c.code, w});
         return w;
     }
     void h2d(void* d, const void* h, size_t bytes) {
@@ -213,7 +247,7 @@ uint32_t flags_from_cfg() {
 SP_result decode_one(const double* llr, const H_matrix& H, const int* syndrome, size_t max_it, double thr,
                      int* out) {
     if (max_it == 0) return {0, false};
-    qkd_code* c = code_for(H);
+    const CodeRef c = code_for(H);
     ThreadCtx& t = ctx();
     const size_t n = H.num_bit_nodes, m = H.num_check_nodes;
     std::vector<uint8_t> syn_h(m), bits_h(n);
@@ -226,7 +260,7 @@ SP_result decode_one(const double* llr, const H_matrix& H, const int* syndrome, 
     t.h2d(d_llr, llr, n * sizeof(double));
     t.h2d(d_syn, syn_h.data(), m);
     const uint32_t cap = (uint32_t)std::min<size_t>(max_it, 0xffffffffu);
-    if (qkd_decode_batch(c, t.workspace(c), d_llr, d_syn, 1, cap, thr, flags_from_cfg(), d_bits, d_it, d_ok,
+    if (qkd_decode_batch(c.get(), t.workspace(c), d_llr, d_syn, 1, cap, thr, flags_from_cfg(), d_bits, d_it, d_ok,
                          t.stream) != QKD_OK)
         fail("qkd_decode_batch");
     uint32_t it = 0;
@@ -240,7 +274,7 @@ SP_result decode_one(const double* llr, const H_matrix& H, const int* syndrome, 
 }
 
 LDPC_result qkd_one(const int* alice, const int* bob, double qber, const H_matrix& H) {
-    qkd_code* c = code_for(H);
+    const CodeRef c = code_for(H);
     ThreadCtx& t = ctx();
     const size_t n = H.num_bit_nodes;
     if (CFG.SUM_PRODUCT_MAX_ITERATIONS == 0) return {{0, false}, false};
@@ -257,7 +291,7 @@ LDPC_result qkd_one(const int* alice, const int* bob, double qber, const H_matri
     t.h2d(d_a, a.data(), n);
     t.h2d(d_b, b.data(), n);
     const uint32_t cap = (uint32_t)std::min<size_t>(CFG.SUM_PRODUCT_MAX_ITERATIONS, 0xffffffffu);
-    if (qkd_qkd_ldpc_batch(c, t.workspace(c), d_a, d_b, 1, qber, cap, CFG.SUM_PRODUCT_MSG_LLR_THRESHOLD,
+    if (qkd_qkd_ldpc_batch(c.get(), t.workspace(c), d_a, d_b, 1, qber, cap, CFG.SUM_PRODUCT_MSG_LLR_THRESHOLD,
                            flags_from_cfg(), nullptr, d_it, d_sp, d_ko, t.stream) != QKD_OK)
         fail("qkd_qkd_ldpc_batch");
     uint32_t it = 0;
@@ -270,7 +304,7 @@ LDPC_result qkd_one(const int* alice, const int* bob, double qber, const H_matri
 }
 
 void syndrome_one(const int* bits, const H_matrix& H, int* out) {
-    qkd_code* c = code_for(H);
+    const CodeRef c = code_for(H);
     ThreadCtx& t = ctx();
     const size_t n = H.num_bit_nodes, m = H.num_check_nodes;
     std::vector<uint8_t> b(n), s(m);
@@ -278,7 +312,7 @@ void syndrome_one(const int* bits, const H_matrix& H, int* out) {
     uint8_t* d_b = t.bits.get(n);
     uint8_t* d_s = t.syn.get(m);
     t.h2d(d_b, b.data(), n);
-    if (qkd_syndrome_batch(c, d_b, 1, d_s, t.stream) != QKD_OK) fail("qkd_syndrome_batch");
+    if (qkd_syndrome_batch(c.get(), d_b, 1, d_s, t.stream) != QKD_OK) fail("qkd_syndrome_batch");
     t.d2h(s.data(), d_s, m);
     t.sync();
     for (size_t j = 0; j < m; ++j) out[j] = s[j];
@@ -294,7 +328,7 @@ std::vector<trial_result> qkd_amd_run_trials(const H_matrix& matrix, double QBER
                                              size_t count, size_t seed_offset) {
     std::vector<trial_result> res(count);
     if (count == 0) return res;
-    qkd_code* c = code_for(matrix);
+    const CodeRef c = code_for(matrix);
     ThreadCtx& t = ctx();
     const size_t chunk = 1u << 18;
     std::vector<uint32_t> it(std::min(count, chunk));
@@ -314,7 +348,7 @@ std::vector<trial_result> qkd_amd_run_trials(const H_matrix& matrix, double QBER
             for (size_t k = 0; k < f; ++k) res[base + k] = {{{0, false}, false}, 0.0};
             continue;
         }
-        const qkd_status s = qkd_trials_batch(c, t.workspace(c), d_seeds, seed_offset, f, QBER, cap,
+        const qkd_status s = qkd_trials_batch(c.get(), t.workspace(c), d_seeds, seed_offset, f, QBER, cap,
                                               CFG.SUM_PRODUCT_MSG_LLR_THRESHOLD, flags_from_cfg(), d_it, d_sp,
                                               d_ko, d_q, nullptr, t.stream);
         if (s == QKD_ERR_QBER_TOO_SMALL)

@@ -233,6 +233,13 @@ QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t 
  * reference counterpart (the reference prints TRACE_* arrays instead,
  * qkd_ldpc_algorithm.cpp:42-155). */
 QKD_API qkd_status qkd_debug_phase_cycles(qkd_workspace *ws, uint64_t *cycles7);
+/* Decoder-kernel timing (the measurement's live roofline figure): start != 0
+ * turns it on for `ws` (zeroed): every later decoder launch on ws is bracketed
+ * by two HIP events on its stream, so only the decode kernel is timed (not the
+ * packing, frame-syndrome or key-compare kernels around it). start == 0
+ * synchronises those events, returns the summed kernel milliseconds and the
+ * number of launches, and turns timing off. No reference counterpart. */
+QKD_API qkd_status qkd_debug_decoder_timing(qkd_workspace *ws, int start, double *ms_total, uint64_t *launches);
 /* Frames of the QKD path (qkd_qkd_ldpc_batch / qkd_trials_batch, binary64
  * rule, clamp on) whose speculative interval iterations could not certify a
  * hard decision (or reached the cap) and were decoded again with the exact

@@ -20,8 +20,19 @@ except Exception:  # pragma: no cover - torch is present in this image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# QKD_AMD_LIB points at another build of the same library (diagnostic builds)
-LIB_PATH = os.environ.get("QKD_AMD_LIB") or os.path.join(_HERE, "lib", "libqkd_ldpc_amd.so")
+LIB_PATH = os.path.join(_HERE, "lib", "libqkd_ldpc_amd.so")
+# A/B experiments only: QKD_AMD_LIB names another build of the same library, and is
+# honoured only together with QKD_AMD_DIAGNOSTIC=1 (with a warning on stderr), so
+# the product path cannot be swapped silently.
+if os.environ.get("QKD_AMD_LIB"):
+    if os.environ.get("QKD_AMD_DIAGNOSTIC") == "1":
+        import sys as _sys
+        LIB_PATH = os.environ["QKD_AMD_LIB"]
+        print(f"qkd_ldpc_amd: DIAGNOSTIC build {LIB_PATH} in place of the product library",
+              file=_sys.stderr)
+    else:
+        raise ImportError("QKD_AMD_LIB is set without QKD_AMD_DIAGNOSTIC=1: refusing to load a "
+                          "library other than the in-tree product build")
 
 # qkd_status
 OK = 0
@@ -52,7 +63,7 @@ EXPORTS = [
     "qkd_keygen_batch", "qkd_trials_batch", "qkd_counters_batch", "qkd_make_seeds",
     "qkd_qber_range", "qkd_debug_phase_cycles", "qkd_debug_spec_replays", "qkd_debug_math", "qkd_debug_phi_sweep", "qkd_trace_decode",
     "qkd_interactive_batch",
-    "qkd_code_from_alist_ex",
+    "qkd_code_from_alist_ex", "qkd_debug_decoder_timing",
 ]
 
 
@@ -115,6 +126,7 @@ def lib():
             "qkd_make_seeds": (st, [U64, SZ, P]),
             "qkd_qber_range": (st, [D, D, D, P, SZ, C.POINTER(SZ)]),
             "qkd_debug_phase_cycles": (st, [P, P]),
+            "qkd_debug_decoder_timing": (st, [P, C.c_int, C.POINTER(D), C.POINTER(U64)]),
             "qkd_debug_spec_replays": (st, [P, P, C.c_int]),
             "qkd_debug_math": (st, [C.c_int, P, P, SZ, P]),
             "qkd_debug_phi_sweep": (st, [C.c_int, C.c_uint32, C.c_uint32, P]),

@@ -291,12 +291,13 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
     // the exact QKD-path shortcuts (first/second-iteration tables) exist for
     // the reference rule only
     constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64 && !GT;
-    constexpr bool MSL = RULE == kRuleMinSumLds;
+    constexpr bool MSL = RULE == kRuleMinSumLds || RULE == kRuleMinSumLdsSc;
+    constexpr bool SC = RULE == kRuleMinSumLdsSc;      // self-corrected min-sum
     static_assert(!(MSL && GT), "the LDS-state min-sum keeps its totals in LDS");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
     const DecodeLds L(c.n_pad, (c.n + 63) / 64, c.m, DC, a.tab2_entries, GT ? 0 : (int)sizeof(T),
-                      MSL ? c.m : 0, (int)sizeof(T), MSL && a.ms_sc);
+                      MSL ? c.m : 0, (int)sizeof(T), SC);
     uint4* cst = reinterpret_cast<uint4*>(smem + L.cst);
     uint32_t* czf = reinterpret_cast<uint32_t*>(smem + L.czf);
     const int m_words = decode_m_words(c.m);
@@ -438,10 +439,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_kernel(DecodeArgs a) {
             if constexpr (MSL) {
                 tabled = true;
                 if (it == 0)
-                    ms_check_phase<kSrcFirst, CLAMP, DC>(c, tsyn, total, cst, czf, a.ms_sc != 0, thr, a.ms_scale,
+                    ms_check_phase<kSrcFirst, CLAMP, DC>(c, tsyn, total, cst, czf, SC, thr, a.ms_scale,
                                                          a.ms_offset);
                 else
-                    ms_check_phase<kSrcGeneral, CLAMP, DC>(c, tsyn, total, cst, czf, a.ms_sc != 0, thr, a.ms_scale,
+                    ms_check_phase<kSrcGeneral, CLAMP, DC>(c, tsyn, total, cst, czf, SC, thr, a.ms_scale,
                                                            a.ms_offset);
             }
             if constexpr (TABLES) {
@@ -880,7 +881,7 @@ static DecodeFn pick_decode_dc(int max_dc, int* dc) {
         if (max_dc <= 6) { *dc = 6; return decode_kernel<MODE, RULE, 6, CLAMP, false>; }
         if (max_dc <= 8) { *dc = 8; return decode_kernel<MODE, RULE, 8, CLAMP, false>; }
         if (max_dc <= 16) { *dc = 16; return decode_kernel<MODE, RULE, 16, CLAMP, false>; }
-        if constexpr (RULE == kRuleMinSumLds) {   // decode_ms_fits: degree <= 32
+        if constexpr (RULE == kRuleMinSumLds || RULE == kRuleMinSumLdsSc) {   // decode_ms_fits: degree <= 32
             *dc = 32;
             return decode_kernel<MODE, RULE, 32, CLAMP, false>;
         } else {
@@ -902,6 +903,8 @@ static DecodeFn pick_decode_rule(int rule, bool clamp, int max_dc, int* dc) {
     if (rule == kRuleMinSum) return pick_decode_clamp<MODE, kRuleMinSum, GT>(clamp, max_dc, dc);
     if constexpr (!GT)
         if (rule == kRuleMinSumLds) return pick_decode_clamp<MODE, kRuleMinSumLds, false>(clamp, max_dc, dc);
+    if constexpr (!GT)
+        if (rule == kRuleMinSumLdsSc) return pick_decode_clamp<MODE, kRuleMinSumLdsSc, false>(clamp, max_dc, dc);
     return pick_decode_clamp<MODE, kRuleSp64, GT>(clamp, max_dc, dc);
 }
 
@@ -929,8 +932,9 @@ static float minsum_scale_of(uint32_t flags) {
 static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries, int rule, bool gt = false,
                                bool sc = false) {
     const int esz = rule == kRuleSp64 ? 8 : 4;
+    const bool msl = rule == kRuleMinSumLds || rule == kRuleMinSumLdsSc;
     return DecodeLds(c->n_pad, (c->n + 63) / 64, c->m, dc, tab2_entries, gt ? 0 : esz,
-                     rule == kRuleMinSumLds ? c->m : 0, esz, rule == kRuleMinSumLds && sc).bytes;
+                     msl ? c->m : 0, esz, msl && sc).bytes;
 }
 
 static constexpr size_t kLdsBytesMax = 160 * 1024;
@@ -1025,6 +1029,7 @@ static qkd_status ws_free(qkd_workspace* ws) {
     if (ws->spec_stat_host) (void)hipHostFree(ws->spec_stat_host);
     if (ws->spec_stat_ev) (void)hipEventDestroy(ws->spec_stat_ev);
     if (ws->done) (void)hipEventDestroy(ws->done);
+    for (hipEvent_t e : ws->dec_ev) (void)hipEventDestroy(e);
     return QKD_OK;
 }
 
@@ -1057,6 +1062,19 @@ struct WsSession {
 
 static unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
+// qkd_debug_decoder_timing: one event recorded on the launch stream before
+// and one after each decoder kernel while timing is on (events pooled per ws)
+static hipError_t decoder_event(qkd_workspace* ws, hipStream_t stream) {
+    if (!ws->time_decoder) return hipSuccess;
+    if (ws->dec_ev_used == ws->dec_ev.size()) {
+        hipEvent_t e = nullptr;
+        const hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        ws->dec_ev.push_back(e);
+    }
+    return hipEventRecord(ws->dec_ev[ws->dec_ev_used++], stream);
+}
+
 static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs& a, int mode,
                                 uint32_t flags, hipStream_t stream) {
     int dc = 0;
@@ -1069,6 +1087,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     if (a.ms_sc && rule != kRuleMinSumLds)
         return set_error(QKD_ERR_UNSUPPORTED, "self-corrected min-sum needs the LDS-state min-sum kernel "
                                               "(check degree <= 32, its state in LDS)");
+    if (a.ms_sc) rule = kRuleMinSumLdsSc;
     a.ms_scale = minsum_scale_of(flags);
     a.ms_offset = (float)((flags >> QKD_MINSUM_OFFSET_SHIFT) & 0xffu) / 64.0f;
     // The split-store kernel (decode_split.hip) for the sum-product rules
@@ -1162,8 +1181,10 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                     a.ckpt_stride = (uint32_t)slots;
                 }
             }
+            QKD_HIP(decoder_event(ws, stream));
             hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
             QKD_HIP(hipGetLastError());
+            QKD_HIP(decoder_event(ws, stream));
             if (mode == kModeKeys) QKD_HIP(launch_key_match(a, stream));
             return QKD_OK;
         }
@@ -1181,7 +1202,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     grid = (int)std::min<size_t>((size_t)grid, a.n_frames);
     // diagnostic: QKD_DECODE_GRID caps the resident workgroups (frames in flight)
     if (const char* g = getenv("QKD_DECODE_GRID")) grid = std::max(1, std::min(grid, atoi(g)));
-    s = ws_reserve_decode(ws, rule == kRuleMinSumLds ? 0 : (size_t)grid);   // no global messages
+    s = ws_reserve_decode(ws, (rule == kRuleMinSumLds || rule == kRuleMinSumLdsSc) ? 0 : (size_t)grid);   // no global messages
     if (s != QKD_OK) return s;
     a.code = c->view();
     a.c2b = ws->c2b;
@@ -1197,8 +1218,10 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
         a.phase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 64);
         QKD_HIP(hipMemsetAsync(a.phase, 0, 64, stream));
     }
+    QKD_HIP(decoder_event(ws, stream));
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kDecodeBlock), lds, stream, a);
     QKD_HIP(hipGetLastError());
+    QKD_HIP(decoder_event(ws, stream));
     return QKD_OK;
 }
 
@@ -1434,8 +1457,9 @@ static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uin
     const char* mode = getenv("QKD_KEYGEN");
     const bool serial = mode && !strcmp(mode, "serial");
     const uint32_t replay = mode && !strcmp(mode, "replay") ? 1u : 0u;
-    if (ne <= kKeygenFastMaxErrors && c->d_jump && !serial) {
-        const size_t lds = (size_t)kKeygenFrames * (2 * (size_t)ne * sizeof(uint32_t) + (ne / 2 + 1) * sizeof(uint2));
+    // (the fast kernel's per-frame LDS times kKeygenFrames must fit a workgroup's LDS)
+    const size_t lds = (size_t)kKeygenFrames * (2 * (size_t)ne * sizeof(uint32_t) + (ne / 2 + 1) * sizeof(uint2));
+    if (ne <= kKeygenFastMaxErrors && c->d_jump && !serial && lds <= kLdsBytesMax) {
         hipLaunchKernelGGL(keygen_fast_kernel, dim3((unsigned)((n_frames + kKeygenFrames - 1) / kKeygenFrames)),
                            dim3(kKeygenBlock), lds, stream, seeds, offset, (uint32_t)c->n, words, (uint32_t)ne,
                            c->keygen_chunk, (uint32_t)n_frames, c->d_jump, ws->alice_w, ws->bob_w, exact_q, replay);
@@ -1515,7 +1539,8 @@ qkd_status qkd_interactive_batch(const qkd_code* c, qkd_workspace* ws, uint64_t 
     uint32_t max_ne = 1;
     size_t run = n_points;
     for (size_t p = 0; p < n_points; ++p) {
-        if (!(q_nominal[p] > 0.0 && q_nominal[p] <= 1.0)) return set_error(QKD_ERR_INVALID_ARG, "QBER must be in (0,1]");
+        // (decoded points: log((1 - q) / q) must be finite, as qkd_qkd_ldpc_batch requires)
+        if (!(q_nominal[p] > 0.0 && q_nominal[p] < 1.0)) return set_error(QKD_ERR_INVALID_ARG, "QBER must be in (0,1)");
         const uint64_t e = qkdr::num_errors((uint32_t)c->n, q_nominal[p]);
         if (e == 0) {
             run = p;
@@ -1855,6 +1880,27 @@ qkd_status qkd_debug_spec_replays(qkd_workspace* ws, uint64_t* replays, int rese
     return QKD_OK;
 }
 
+qkd_status qkd_debug_decoder_timing(qkd_workspace* ws, int start, double* ms_total, uint64_t* launches) {
+    if (!ws) return set_error(QKD_ERR_INVALID_ARG, "null workspace");
+    DeviceGuard g(ws->device);
+    std::lock_guard<std::mutex> lk(ws->mu);
+    double tot = 0.0;
+    const size_t pairs = ws->dec_ev_used / 2;
+    if (!start) {
+        for (size_t k = 0; k < pairs; ++k) {
+            QKD_HIP(hipEventSynchronize(ws->dec_ev[2 * k + 1]));
+            float ms = 0.0f;
+            QKD_HIP(hipEventElapsedTime(&ms, ws->dec_ev[2 * k], ws->dec_ev[2 * k + 1]));
+            tot += ms;
+        }
+    }
+    if (ms_total) *ms_total = tot;
+    if (launches) *launches = start ? 0 : pairs;
+    ws->dec_ev_used = 0;
+    ws->time_decoder = start != 0;
+    return QKD_OK;
+}
+
 qkd_status qkd_debug_phase_cycles(qkd_workspace* ws, uint64_t* cycles7) {
     if (!ws || !cycles7) return set_error(QKD_ERR_INVALID_ARG, "null argument");
     if (!ws->counter) return set_error(QKD_ERR_INVALID_ARG, "workspace has not decoded yet");
@@ -1890,6 +1936,8 @@ qkd_status qkd_trials_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t
     qkd_status s = check_frames(n_frames);
     if (s == QKD_OK) s = check_decode_params(max_iterations, msg_threshold, flags);
     if (s != QKD_OK) return s;
+    // (the keys are decoded: log((1 - q) / q) must be finite, as qkd_qkd_ldpc_batch requires)
+    if (!(q_nominal > 0.0 && q_nominal < 1.0)) return set_error(QKD_ERR_INVALID_ARG, "QBER must be in (0,1)");
     DeviceGuard g(c->device);
     ws = resolve_ws(c, ws);
     if (!ws) return set_error(QKD_ERR_OUT_OF_MEMORY, "no workspace");

@@ -42,7 +42,7 @@ namespace qkd {
 template <int DC>
 struct SegWeights {
     const float* w;         // DC <= 8: wtab row of (deg, p)
-    uint32_t mask;          // otherwise: bit k = weight of entry k
+    uint64_t mask;          // otherwise: bit k = weight of entry k
     __device__ __forceinline__ SegWeights(const float* wtab, int deg, int p) {
         if constexpr (DC <= 8) {
             // (idle lanes: a degree-1 segment starting at lane 0, p = lane;
@@ -50,13 +50,16 @@ struct SegWeights {
             w = wtab + ((deg - 1) * DC + min(p, DC - 1)) * DC;
             mask = 0;
         } else {
+            // 64-bit: deg reaches 64 in the widest bucket and p (= lane - start)
+            // any lane 0..63 for idle lanes; both shifts stay below 64
             w = nullptr;
-            mask = ((1u << deg) - 1u) & ~(1u << (uint32_t)p);
+            const uint64_t seg = deg >= 64 ? ~0ull : ((1ull << (uint32_t)deg) - 1ull);
+            mask = seg & ~(1ull << ((uint32_t)p & 63u));
         }
     }
     __device__ __forceinline__ float operator[](int k) const {
         if constexpr (DC <= 8) return w[k];
-        else return (float)((mask >> k) & 1u);
+        else return (float)(uint32_t)((mask >> (uint32_t)k) & 1ull);
     }
 };
 
@@ -266,7 +269,8 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
             const bool ok = i < c.n;
             bc[u] = ok ? c.bit_code[i] : 0;
 #pragma unroll
-            for (int k = 0; k < kDvUnroll; ++k) v[u][k] = (FOLD || !ok) ? 0.0f : ms.ld((uint32_t)k * n_pad + i);
+            for (int k = 0; k < kDvUnroll; ++k)     // (rows past max_dv have no slots)
+                v[u][k] = (FOLD || !ok || k >= c.max_dv) ? 0.0f : ms.ld((uint32_t)k * n_pad + i);
         }
 #pragma unroll
         for (int u = 0; u < kSp32Chunk; ++u) {

@@ -43,7 +43,10 @@ enum DecodeMode : int {
 //   kRuleMinSumLds  the same min-sum with the frame's whole message state in
 //               LDS (per check: min1, min2, argmin, sign bits), no global
 //               message store; used when the state fits (decode_ms_fits)
-enum DecodeRule : int { kRuleSp64 = 0, kRuleSp32 = 1, kRuleMinSum = 2, kRuleMinSumLds = 3 };
+//   kRuleMinSumLdsSc  kRuleMinSumLds with Savin's self-correction
+//               (QKD_MINSUM_SELF_CORRECT) compiled in: its own kernel
+//               instantiation, so profiles attribute its time to it
+enum DecodeRule : int { kRuleSp64 = 0, kRuleSp32 = 1, kRuleMinSum = 2, kRuleMinSumLds = 3, kRuleMinSumLdsSc = 4 };
 template <int RULE> struct RuleMsg { using T = float; };
 template <> struct RuleMsg<kRuleSp64> { using T = double; };
 

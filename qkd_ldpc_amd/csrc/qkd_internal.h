@@ -119,6 +119,11 @@ struct qkd_workspace {
     // checkpointed speculation: one saved message store per resident workgroup
     double* ckpt = nullptr;
     size_t ckpt_slots = 0;
+    // qkd_debug_decoder_timing: while on, HIP events bracket every decoder
+    // launch on its stream (pairs recorded, read back on collection)
+    bool time_decoder = false;
+    std::vector<hipEvent_t> dec_ev;        // start, stop, start, stop, ...
+    size_t dec_ev_used = 0;
 };
 
 struct qkd_code {

@@ -7,8 +7,26 @@ exchanged on the data path. The per-point counters of simulation.cpp:252-312
 all-reduce each for the sums (SUM) and the extrema (MIN / MAX), over RCCL on
 MI355X (backend "nccl") or gloo on CPU. The integer sums make the combined
 mean/std independent of the rank count.
+
+This replaces the reference's thread-pool fan-out of a point's trials
+(simulation.cpp:230-250, `detach_loop` over THREADS_NUMBER threads): ranks
+take the place of pool threads, a frame queue inside each rank's decoder the
+place of the per-trial tasks.
+
+Launching: `spawn_ranks` starts N copies of a script as ranks 0..N-1 (the
+environment torchrun would give them: RANK, LOCAL_RANK, WORLD_SIZE,
+MASTER_ADDR=127.0.0.1, MASTER_PORT) and makes no HIP call itself, so the
+parent never initialises a GPU; `init_rank` is each rank's side: it checks the
+world against the visible devices (one device per rank for RCCL; gloo may
+share one), binds the device and opens the process group.
 """
 from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+import time
 
 
 def shard_range(rank: int, world: int, frames: int) -> tuple[int, int]:
@@ -37,3 +55,92 @@ def allreduce_counters(counters, group=None):
     ext[0:1] = mn.to(torch.int32)                   # two's-complement store keeps the uint32 bits
     ext[1:2] = mx.to(torch.int32)
     return counters
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(world: int, argv: list[str], env_extra: dict | None = None, poll_s: float = 0.2) -> int:
+    """Run `python argv...` as ranks 0..world-1 on this node and wait for them.
+
+    Each rank gets the torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT). Their stdout/stderr
+    are this process's. If one rank fails, the others (which would wait in a
+    collective) are terminated, by their exact PIDs. Returns the first non-zero
+    exit status, else 0. No GPU call is made here."""
+    if world < 1:
+        raise ValueError(f"world size must be >= 1, got {world}")
+    port = free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.update(env_extra or {})
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
+    status = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc
+                    for q in live:
+                        q.terminate()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return status
+
+
+def rank_env() -> tuple[int, int, int] | None:
+    """(rank, world, local_rank) from a torchrun / spawn_ranks environment, or None."""
+    if "WORLD_SIZE" not in os.environ:
+        return None
+    return (int(os.environ.get("RANK", "0")), int(os.environ["WORLD_SIZE"]),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init_rank(world: int, local: int, backend: str | None = None, use_gpu: bool = True):
+    """This rank's side of the launch: bind the device and open the process group.
+
+    backend: "nccl" (RCCL, the default with a GPU) needs one visible device per
+    rank on the node and fails loudly otherwise; "gloo" lets ranks share
+    devices (local % visible) and runs without a GPU (use_gpu=False: CPU
+    tensors, tests). Returns the torch.device this rank works on."""
+    import torch
+    import torch.distributed as dist
+
+    backend = backend or os.environ.get("QKD_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+    if backend not in ("nccl", "gloo"):
+        raise RuntimeError(f"QKD_DIST_BACKEND must be nccl or gloo, got {backend!r}")
+    dev = torch.device("cpu")
+    if use_gpu:
+        n_dev = torch.cuda.device_count()
+        if n_dev < 1:
+            raise RuntimeError("no visible GPU for this rank")
+        if backend == "nccl" and local >= n_dev:
+            raise RuntimeError(f"world size {world}: local rank {local} has no GPU of its own "
+                               f"({n_dev} visible; RCCL needs one device per rank, "
+                               "QKD_DIST_BACKEND=gloo shares them)")
+        dev = torch.device("cuda", local % n_dev)
+        torch.cuda.set_device(dev)
+    elif backend == "nccl":
+        raise RuntimeError("the nccl (RCCL) backend needs GPUs")
+    if world > 1 or backend == "nccl":
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return dev

@@ -63,3 +63,60 @@ def test_counter_allreduce_matches_single_process(world):
     want = counters_of(iters, sp, ko).tobytes()
     for r in range(world):
         assert out[r] == want
+
+
+# ---- the launcher (qkd_ldpc_amd.dist.spawn_ranks / init_rank) and bench.py's use of it ----
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_spawned_ranks_reduce_to_single_rank_counters(tmp_path, oracle_mod, golden_code):
+    """Two ranks started by spawn_ranks (the path `bench.py --gpus 2` takes without
+    torchrun) shard 24 config-2 frames, decode their shares and all-reduce the counters
+    over gloo: rank 0's record equals one process's record over all 24 frames."""
+    from qkd_ldpc_amd.dist import spawn_ranks
+    out = str(tmp_path / "r.json")
+    frames, q = 24, 0.02
+    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "dist_rehearsal.py"), out, str(frames), str(q)])
+    assert rc == 0
+    import json
+    got = json.load(open(out))
+    code = oracle_mod.Code.from_lists(golden_code)
+    r = code.trials(q, oracle_mod.seeds(777, frames), 0, 50, 100.0, True, threads=2)
+    want = counters_of(np.asarray(r["iters"], np.uint32), np.asarray(r["sp_ok"], np.uint8),
+                       np.asarray(r["key_ok"], np.uint8))
+    assert got["world"] == 2 and got["frames"] == frames
+    assert bytes(got["counters"]) == want.tobytes()
+
+
+def test_spawn_ranks_propagates_a_failed_rank(tmp_path):
+    """A rank that dies makes the launcher fail (its peer, waiting in a collective,
+    is terminated rather than left hanging)."""
+    from qkd_ldpc_amd.dist import spawn_ranks
+    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "dist_rehearsal.py"), str(tmp_path / "x.json"), "4",
+                         "0.02", "1"])
+    assert rc != 0
+
+
+def _bench(args, env_extra=None, timeout=300):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_gpus_disagreeing_with_world_size_fails():
+    p = _bench(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0",
+                                 "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29599"})
+    assert p.returncode != 0 and "disagrees" in p.stderr
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure")
+def test_bench_gpus_two_without_gpus_fails_loudly():
+    """`bench.py --gpus 2` with no torchrun starts two ranks itself; here (no GPU) each
+    rank must refuse to run rather than decode elsewhere."""
+    p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert p.returncode != 0
+    assert "no visible GPU" in p.stderr

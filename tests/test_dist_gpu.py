@@ -1,0 +1,51 @@
+"""The multi-GPU path on the MI355X: RCCL itself (a world-size-1 "nccl" process
+group all-reducing real counter records, the collective bench.py issues per step)
+and `bench.py --gpus 2` starting its own ranks (gloo sharing the one device: RCCL
+needs one GPU per rank). Replaces the reference's thread-pool fan-out of a point's
+trials (simulation.cpp:230-250)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def test_rccl_allreduce_of_real_counters(tmp_path):
+    from qkd_ldpc_amd.dist import spawn_ranks
+    out = str(tmp_path / "nccl.json")
+    rc = spawn_ranks(1, [os.path.join(ROOT, "tests", "dist_gpu_rank.py"), out])
+    assert rc == 0
+    res = json.load(open(out))
+    assert res["backend"] == "nccl" and res["world"] == 1
+    assert res["same_ok"], "a one-rank all-reduce must leave the counters unchanged"
+    assert res["same_failed"] and res["failed_minmax"] == [0xFFFFFFFF, 0]
+    c = np.array(res["counters"], np.uint8)
+    sums = c[:40].view(np.uint64)
+    assert sums[0] == 512 and sums[1] == 512 and sums[2] == 512
+
+
+def test_bench_starts_its_own_ranks(golden_vectors):
+    """`python bench.py --gpus 2` (no torchrun): two ranks on the one MI355X over gloo,
+    each decoding its 512-frame share of the seed stream; the reduced counters are the
+    golden per-frame outcomes of frames 0..1023."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["QKD_DIST_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--frames", "512", "--no-e2e", "--no-variants", "--no-cpu-baseline",
+                        "--no-sweeps"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, p.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 2
+    it = golden_vectors["c2_iters"][:1024].astype(np.int64)
+    sp = golden_vectors["c2_sp"][:1024].astype(bool)
+    assert out["sum_iterations"] == int(it[sp].sum())
+    assert out["fer"] == 0.0
+    assert abs(out["value"] - 2 * 512 * 10240 * 2 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 1e-6

@@ -181,6 +181,19 @@ def test_qber_too_small_raises(Q, H):
     assert "too small" in str(ei.value)
 
 
+def test_decoded_qber_of_one_rejected(Q, H):
+    """Key generation accepts q = 1 (every bit flipped), but a decoded point needs a
+    finite log((1 - q) / q): trials and interactive mode reject q >= 1 as
+    qkd_qkd_ldpc_batch does, before any key is drawn."""
+    seeds = seeds_dev(np.arange(4, dtype=np.uint64))
+    with pytest.raises(Q.QkdError) as ei:
+        Q.run_trials(H, seeds, 1.0)
+    assert ei.value.status == Q._native.ERR_INVALID_ARG
+    with pytest.raises(Q.QkdError) as ei:
+        Q.interactive_simulation(H, 777, [0.02, 1.0])
+    assert ei.value.status == Q._native.ERR_INVALID_ARG
+
+
 # ---- fused trials: BASELINE configs 2 and 3 per frame ----------------------------------
 
 def test_trials_config2_full_batch(Q, H, probe, golden_vectors):

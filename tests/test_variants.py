@@ -334,3 +334,81 @@ def test_variant_trials_counters(Q, H):
     ko = r.keys_match.cpu().numpy().astype(bool)
     assert c.frames == 512 and c.sp_ok == sp.sum() and c.ldpc_ok == (sp & ko).sum()
     assert c.sum_iters == it[sp].sum()
+
+
+# ---- high-rate codes: check degrees in the 16 and 64 buckets -------------------------------
+
+def _high_rate_code(n, dc, seed):
+    """(3, dc)-regular code: each bit (random order) joins the three distinct checks
+    with the most free places (random tie-break), so no edge repeats and every
+    check ends with exactly dc bits. -> (m, check_ptr, check_idx), rows ascending."""
+    rng = np.random.default_rng(seed)
+    m = n * 3 // dc
+    assert m * dc == n * 3
+    free = np.full(m, dc)
+    rows = [[] for _ in range(m)]
+    for i in rng.permutation(n):
+        key = free + rng.random(m) * 0.5
+        for j in np.argsort(-key)[:3]:
+            rows[j].append(int(i))
+            free[j] -= 1
+    assert (free == 0).all()
+    ci = np.concatenate([sorted(r) for r in rows]).astype(np.int32)
+    return m, np.arange(0, m * dc + 1, dc, dtype=np.int32), ci
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,dc,q", [(2048, 64, 0.002), (2048, 32, 0.005), (1536, 12, 0.02)])
+@pytest.mark.parametrize("path", ["llr", "keys"])
+def test_sp_f32_high_check_degree_bit_exact(Q, oracle_mod, n, dc, q, path):
+    """sp_f32 on codes whose check degree lands in the 16- and 64-entry buckets of the
+    check phase (R = 0.95 at degree 64, the reference config's code_rate 0.95 row):
+    the extrinsic-sum weights of those buckets come from a 64-bit segment mask
+    (decode_split.hip SegWeights); bit for bit against the specification."""
+    from oracle.variants import sp_f32_decode
+    m, cp, ci = _high_rate_code(n, dc, seed=dc)
+    model = MinSumModel(n, m, cp, ci)
+    Hh = Q.HMatrix.from_check_lists(n, cp, ci)
+    assert Hh.max_check_nodes_weight == dc
+    A, B = [], []
+    for s in oracle_mod.seeds(dc + 5, 16):
+        a, b, qq = oracle_mod.keygen(int(s), n, q)
+        A.append(a)
+        B.append(b)
+    A, B = np.array(A, np.uint8), np.array(B, np.uint8)
+    lp = np.log((1 - qq) / qq)
+    llr = np.where(B == 1, -lp, lp)
+    syn = model.syndrome(A)
+    if path == "llr":
+        r = Q.sum_product_decoding(Hh, _dev(llr, np.float64), _dev(syn, np.uint8), 30, 100.0, True,
+                                   variant="sp_f32")
+    else:
+        r = Q.qkd_ldpc(Hh, _dev(A, np.uint8), _dev(B, np.uint8), float(qq), 30, 100.0, True,
+                       want_bits=True, variant="sp_f32")
+    torch.cuda.synchronize()
+    wb, wi, wo = sp_f32_decode(model, llr, syn, 30, 100.0, True,
+                               tanh_half=_dev_math(2), two_atanh=_dev_math(3))
+    assert (r.iterations.cpu().numpy() == wi).all()
+    assert (r.syndromes_match.cpu().numpy() == wo).all()
+    assert (r.bits.cpu().numpy() == wb).all()
+    assert wo.mean() > 0.5       # the frames mostly decode: the check phase's sums matter
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,dc,q", [(2048, 64, 0.002), (1536, 12, 0.02)])
+def test_sp_f64_high_check_degree_matches_oracle(Q, oracle_mod, tmp_path, n, dc, q):
+    """The reference decoder on the same high-rate codes: fused trials equal the oracle."""
+    from conftest import write_alist
+    m, cp, ci = _high_rate_code(n, dc, seed=dc)
+    Hh = Q.HMatrix.from_check_lists(n, cp, ci)
+    cptr, cidx, bptr, bidx = Hh.adjacency()
+    p = str(tmp_path / "hr.alist")
+    write_alist(p, n, m, bptr, bidx, cptr, cidx)
+    oc = oracle_mod.Code.from_alist(p)
+    seeds = oracle_mod.seeds(41, 24)
+    r = Q.run_trials(Hh, torch.from_numpy(seeds.view(np.int64)).cuda(), q, 0, 30)
+    torch.cuda.synchronize()
+    want = oc.trials(q, seeds, 0, 30, 100.0, True)
+    assert (r.iterations.cpu().numpy() == want["iters"]).all()
+    assert (r.syndromes_match.cpu().numpy().astype(bool) == want["sp_ok"]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == want["key_ok"]).all()

@@ -1,0 +1,84 @@
+// Microbenchmark (diagnostic, not product): VALU issue cost per wave64
+// instruction per SIMD on gfx950, in shader cycles (s_memtime ticks, read in
+// the kernel), against waves per SIMD and independent chains per lane. Settles
+// the VALU ceiling DESIGN.md §4.3 prices the decoder against: the guide's
+// "2 cycles per wave64 v_fma_f32 (SIMD-32)" vs the 4-cycle single-wave issue.
+//   ./issue_mb            -> one line per (op, waves/SIMD, ILP)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int OP, int ILP>
+__global__ __launch_bounds__(1024) void k(float* out, unsigned long long* cyc, int iters, float a, float b) {
+    float x[ILP];
+    f2 y[ILP];
+    double d[ILP];
+    for (int u = 0; u < ILP; ++u) {
+        x[u] = threadIdx.x * 1e-6f + u * 0.1f + 0.5f;
+        y[u] = f2{x[u], x[u] + 0.25f};
+        d[u] = (double)x[u];
+    }
+    __syncthreads();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < ILP; ++u) {
+            // inline asm: exactly one instruction of the kind under test each
+            // (the compiler would otherwise pack pairs of scalar FMAs)
+            if constexpr (OP == 0) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[u]) : "v"(a), "v"(b));
+            if constexpr (OP == 1) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(y[u]) : "v"(y[0]), "v"(y[1]));
+            if constexpr (OP == 2) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(d[u]) : "v"(d[0]), "v"(d[1]));
+            if constexpr (OP == 3) asm volatile("v_mul_f64 %0, %1, %0" : "+v"(d[u]) : "v"(d[0]));
+            if constexpr (OP == 4) asm volatile("v_add_f64 %0, %1, %0" : "+v"(d[u]) : "v"(d[0]));
+            if constexpr (OP == 5) asm volatile("v_exp_f32 %0, %0" : "+v"(x[u]));
+            if constexpr (OP == 6) asm volatile("v_add_f32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+        }
+    }
+    __syncthreads();
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    float s = 0;
+    for (int u = 0; u < ILP; ++u) s += x[u] + y[u].x + y[u].y + (float)d[u];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int OP, int ILP>
+void run(const char* name, float* d, unsigned long long* dc, int cus, int block, int per_cu) {
+    const int iters = 4096;
+    const int grid = cus * per_cu;
+    hipLaunchKernelGGL((k<OP, ILP>), dim3(grid), dim3(block), 0, 0, d, dc, iters, 0.999f, 1e-7f);
+    hipLaunchKernelGGL((k<OP, ILP>), dim3(grid), dim3(block), 0, 0, d, dc, iters, 0.999f, 1e-7f);
+    hipDeviceSynchronize();
+    static unsigned long long h[8192];
+    hipMemcpy(h, dc, grid * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    double avg = 0;
+    for (int i = 0; i < grid; ++i) avg += (double)h[i];
+    avg /= grid;
+    // waves per SIMD (all workgroups of a CU co-resident: per_cu * block / 64 / 4)
+    const double wps = (double)per_cu * block / 64.0 / 4.0;
+    const double inst = wps * iters * ILP;     // wave-instructions per SIMD
+    printf("%-14s waves/SIMD %4.1f  ILP %d  cycles/wave-inst/SIMD %6.2f\n", name, wps, ILP, avg / inst);
+}
+
+int main() {
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    float* d;
+    unsigned long long* dc;
+    hipMalloc(&d, (size_t)cus * 2 * 1024 * sizeof(float));
+    hipMalloc(&dc, (size_t)cus * 2 * sizeof(unsigned long long));
+    // (block, per_cu): 1, 2, 4, 8 waves per SIMD
+    const int cfg[4][2] = {{256, 1}, {512, 1}, {1024, 1}, {1024, 2}};
+    for (auto& c : cfg) {
+        run<0, 1>("v_fma_f32", d, dc, cus, c[0], c[1]);
+        run<0, 8>("v_fma_f32", d, dc, cus, c[0], c[1]);
+        run<1, 8>("v_pk_fma_f32", d, dc, cus, c[0], c[1]);
+        run<2, 1>("v_fma_f64", d, dc, cus, c[0], c[1]);
+        run<2, 8>("v_fma_f64", d, dc, cus, c[0], c[1]);
+        run<3, 8>("v_mul_f64", d, dc, cus, c[0], c[1]);
+        run<4, 8>("v_add_f64", d, dc, cus, c[0], c[1]);
+        run<5, 8>("v_exp_f32", d, dc, cus, c[0], c[1]);
+        run<6, 8>("v_add_f32", d, dc, cus, c[0], c[1]);
+    }
+    return 0;
+}

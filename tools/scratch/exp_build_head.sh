@@ -1,7 +1,7 @@
 # Build the library of a git revision (default HEAD) into exp_libs/<name>/ for
 # tools/gpu_ab_libs.sh (scratch, git-ignored): exp_build_head.sh [rev] [name]
 set -eu
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 REV=${1:-HEAD}
 NAME=${2:-head}
 TMP=$(mktemp -d)

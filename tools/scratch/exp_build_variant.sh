@@ -3,7 +3,7 @@
 #   exp_build_variant.sh <name> <patch-script.py> [make vars...]
 # The patch script gets the scratch csrc directory as its argument.
 set -eu
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 NAME=$1; PATCH=$2; shift 2
 TMP=$(mktemp -d)
 mkdir -p "$TMP/qkd_ldpc_amd"

@@ -3,7 +3,7 @@
 # Each GPU step has its own time limit; a crash/abort/timeout (rc >= 2 other than
 # an ordinary pytest failure) ends the script before any further GPU step.
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 # Multi-rank rehearsal of bench.py on one GPU: two ranks over gloo sharing the
 # device (the RCCL collective itself needs one GPU per rank).
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 QKD_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

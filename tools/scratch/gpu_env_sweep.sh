@@ -1,10 +1,10 @@
 # Bench under environment settings (one per line of $SWEEP, "name VAR=value ...",
-# e.g. QKD_AMD_LIB=exp_libs/head/libqkd_ldpc_amd.so for another build), the
+# e.g. QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=exp_libs/head/libqkd_ldpc_amd.so for another build), the
 # whole list REPS times. Optional parity subset first ($PARITY_K, a pytest -k
 # expression run with the in-tree library). Each GPU step time-limited; a
 # crash or timeout ends the script.
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 REPS=${REPS:-1}

@@ -1,7 +1,7 @@
 # Round-end check on one GPU: the whole -m gpu suite, smoke, the headline bench
 # (with the CPU baseline), the config-4 per-rank share (125,000 frames).
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?

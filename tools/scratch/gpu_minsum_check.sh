@@ -1,7 +1,7 @@
 # GPU check of the min-sum variants: their bit-exact tests, then the FER sweep of
 # plain and self-corrected min-sum over scales at config 3's hardest points.
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_variants.py -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_minsum.log 2>&1; rc=$?

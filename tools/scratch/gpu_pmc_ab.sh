@@ -4,7 +4,7 @@ mkdir -p gpurun_out/pmcab
 export TMPDIR=/tmp
 timeout -k 10 60 rocprofv3 --list-avail > gpurun_out/pmcab/avail.txt 2>&1 || true
 for l in head pair; do
-  if [ $l = head ]; then export QKD_AMD_LIB=exp_libs/head/libqkd_ldpc_amd.so; else unset QKD_AMD_LIB; fi
+  if [ $l = head ]; then export QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=exp_libs/head/libqkd_ldpc_amd.so; else unset QKD_AMD_LIB; fi
   k=0
   while read -r grp; do
     k=$((k+1))

@@ -1,6 +1,6 @@
 # PMC of the headline decoder at full occupancy and with QKD_DECODE_GRID capped
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/pmcgrid
 export TMPDIR=/tmp
 for g in ${GRIDS:-256 128}; do

@@ -6,7 +6,7 @@
 #     domains) over a short bench of that variant -> $OUT/pmc_<variant>.json
 # Each step has its own time limit; any failure ends the script.
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=${OUT:-gpurun_out/r02prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # bench with per-phase clocks. Each GPU step under its own time limit; a crash,
 # abort or timeout ends the script.
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TESTS=${TESTS:-tests}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Run bench.py once per value of an environment knob: VAR="1 2 3" tools/gpu_sweep.sh NAME
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 name=$1; shift

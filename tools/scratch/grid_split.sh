@@ -2,7 +2,7 @@
 # Diagnostic: decode time vs resident workgroups (QKD_DECODE_GRID) for the
 # split decoder, binary64 and binary32 rules, and vs the LDS budget.
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 for v in sp_f64 sp_f32; do

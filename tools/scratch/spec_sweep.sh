@@ -3,7 +3,7 @@
 # iterations (QKD_SPEC_CAP=0), across QBER; the default policy decides between
 # speculating from the first iteration and from a checkpoint (decode_keys).
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 for q in ${QS:-0.02 0.03 0.04 0.05 0.06 0.07 0.08}; do
