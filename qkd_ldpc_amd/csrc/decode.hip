@@ -621,8 +621,10 @@ __global__ void syndrome_kernel(DeviceCode c, const uint8_t* bits, uint32_t n_fr
 // One lane per 8 key bytes -> one packed byte (little-endian words, so the
 // byte array is the uint64 word array); bits past n are 0. 8-byte loads when
 // every frame row is 8-byte aligned (n % 8 == 0), byte loads otherwise.
-__global__ void pack_kernel(const uint8_t* bytes, uint32_t n, uint32_t words, uint32_t n_frames,
-                            uint64_t* out) {
+__global__ void pack_kernel(const uint8_t* bytes0, const uint8_t* bytes1, uint32_t n, uint32_t words,
+                            uint32_t n_frames, uint64_t* out0, uint64_t* out1) {
+    const uint8_t* bytes = blockIdx.y ? bytes1 : bytes0;
+    uint64_t* out = blockIdx.y ? out1 : out0;
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t per_frame = (size_t)words * 8;
     if (gid >= (size_t)n_frames * per_frame) return;
@@ -700,6 +702,7 @@ __global__ void keygen_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n
 __global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
                                                          uint32_t words, uint32_t ne, uint32_t chunk,
                                                          uint32_t n_frames, const uint64_t* __restrict__ jump,
+                                                         const uint64_t* __restrict__ jpoly,
                                                          uint64_t* alice_w, uint64_t* bob_w, double* exact_q,
                                                          uint32_t force_serial) {
     extern __shared__ uint32_t kg_lds[];
@@ -723,11 +726,18 @@ __global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_
     qkdr::Xoshiro256pp g;
     g.seed(live ? seeds[f] + offset : 0);
     uint64_t st[4] = {g.s0, g.s1, g.s2, g.s3};
-    for (int b = 0; b < kKeygenLevels; ++b) {
-        uint64_t t[4] = {st[0], st[1], st[2], st[3]};
-        qkdr::jump_apply(jump + (size_t)b * 1024, t);
-        if ((lane >> b) & 1u) {
-            st[0] = t[0]; st[1] = t[1]; st[2] = t[2]; st[3] = t[3];
+    if (jpoly) {
+        // the lane's jump as a polynomial in T (qkd_rng.h jump_poly_apply):
+        // 256 state steps, no matrix reads
+        const uint64_t p[4] = {jpoly[lane * 4 + 0], jpoly[lane * 4 + 1], jpoly[lane * 4 + 2], jpoly[lane * 4 + 3]};
+        qkdr::jump_poly_apply(p, st);
+    } else {
+        for (int b = 0; b < kKeygenLevels; ++b) {
+            uint64_t t[4] = {st[0], st[1], st[2], st[3]};
+            qkdr::jump_apply(jump + (size_t)b * 1024, t);
+            if ((lane >> b) & 1u) {
+                st[0] = t[0]; st[1] = t[1]; st[2] = t[2]; st[3] = t[3];
+            }
         }
     }
     g.s0 = st[0]; g.s1 = st[1]; g.s2 = st[2]; g.s3 = st[3];
@@ -860,10 +870,68 @@ __global__ void counters_kernel(const uint32_t* iters, const uint8_t* sp, const 
     }
 }
 
+// One workgroup over every frame (batches up to kCountersOneBlock frames): the
+// reduction and the record's initialisation in one launch.
+constexpr uint32_t kCountersOneBlock = 1u << 16;
+__global__ __launch_bounds__(1024) void counters_one_kernel(const uint32_t* iters, const uint8_t* sp,
+                                                            const uint8_t* ko, uint32_t n_frames,
+                                                            qkd_counters* out) {
+    __shared__ unsigned long long s_sum[5];
+    __shared__ uint32_t s_min, s_max;
+    if (threadIdx.x < 5) s_sum[threadIdx.x] = 0;
+    if (threadIdx.x == 0) { s_min = 0xffffffffu; s_max = 0; }
+    __syncthreads();
+    unsigned long long c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+    uint32_t mn = 0xffffffffu, mx = 0;
+    for (uint32_t f = threadIdx.x; f < n_frames; f += blockDim.x) {
+        if (sp[f]) {
+            const unsigned long long it = iters[f];
+            c1++;
+            if (!ko || ko[f]) c2++;
+            c3 += it;
+            c4 += it * it;
+            mn = min(mn, (uint32_t)it);
+            mx = max(mx, (uint32_t)it);
+        }
+    }
+    atomicAdd(&s_sum[1], c1);
+    atomicAdd(&s_sum[2], c2);
+    atomicAdd(&s_sum[3], c3);
+    atomicAdd(&s_sum[4], c4);
+    atomicMin(&s_min, mn);
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out->frames = n_frames;
+        out->sp_ok = s_sum[1];
+        out->ldpc_ok = s_sum[2];
+        out->sum_iters = s_sum[3];
+        out->sum_iters_sq = s_sum[4];
+        out->min_iters = s_min;
+        out->max_iters = s_max;
+    }
+}
+
+// counters <- the reduction of F frames' outputs (one launch up to kCountersOneBlock)
+static hipError_t launch_counters(const uint32_t* iters, const uint8_t* sp, const uint8_t* ko, size_t n_frames,
+                                  qkd_counters* c, hipStream_t stream);
+
 __global__ void counters_init_kernel(qkd_counters* c) {
     c->frames = c->sp_ok = c->ldpc_ok = c->sum_iters = c->sum_iters_sq = 0;
     c->min_iters = 0xffffffffu;
     c->max_iters = 0;
+}
+
+static hipError_t launch_counters(const uint32_t* iters, const uint8_t* sp, const uint8_t* ko, size_t n_frames,
+                                  qkd_counters* c, hipStream_t stream) {
+    if (n_frames <= kCountersOneBlock) {
+        hipLaunchKernelGGL(counters_one_kernel, dim3(1), dim3(1024), 0, stream, iters, sp, ko, (uint32_t)n_frames, c);
+    } else {
+        hipLaunchKernelGGL(counters_init_kernel, dim3(1), dim3(1), 0, stream, c);
+        hipLaunchKernelGGL(counters_kernel, dim3((unsigned)((n_frames + 255) / 256)), dim3(256), 0, stream, iters, sp,
+                           ko, (uint32_t)n_frames, c);
+    }
+    return hipGetLastError();
 }
 
 // ---- launch plumbing --------------------------------------------------------
@@ -1433,10 +1501,9 @@ qkd_status qkd_qkd_ldpc_batch(const qkd_code* c, qkd_workspace* ws, const uint8_
     if (s != QKD_OK) return s;
     const uint32_t words = (uint32_t)((c->n + 63) / 64);
     const size_t nw = n_frames * words;
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 8, 256)), dim3(256), 0, (hipStream_t)stream, alice,
-                       (uint32_t)c->n, words, (uint32_t)n_frames, ws->alice_w);
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 8, 256)), dim3(256), 0, (hipStream_t)stream, bob,
-                       (uint32_t)c->n, words, (uint32_t)n_frames, ws->bob_w);
+    // Alice's and Bob's keys in one launch (grid.y selects the key)
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 8, 256), 2), dim3(256), 0, (hipStream_t)stream, alice, bob,
+                       (uint32_t)c->n, words, (uint32_t)n_frames, ws->alice_w, ws->bob_w);
     QKD_HIP(hipGetLastError());
     return decode_keys(c, ws, n_frames, qber, max_iterations, msg_threshold, flags, bits_out, iterations,
                        syndromes_match, keys_match, (hipStream_t)stream);
@@ -1453,16 +1520,20 @@ static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uin
     if (s != QKD_OK) return s;
     const uint32_t words = (uint32_t)((c->n + 63) / 64);
     // QKD_KEYGEN=serial forces the one-thread-per-frame kernel, QKD_KEYGEN=replay
-    // the fast kernel's in-wave serial path for every frame (tests of both).
+    // the fast kernel's in-wave serial path for every frame, QKD_KEYGEN=matrix
+    // the fast kernel with its lane jumps as GF(2) matrix products instead of
+    // polynomials (tests of all three).
     const char* mode = getenv("QKD_KEYGEN");
     const bool serial = mode && !strcmp(mode, "serial");
     const uint32_t replay = mode && !strcmp(mode, "replay") ? 1u : 0u;
+    const bool matrix = mode && !strcmp(mode, "matrix");
     // (the fast kernel's per-frame LDS times kKeygenFrames must fit a workgroup's LDS)
     const size_t lds = (size_t)kKeygenFrames * (2 * (size_t)ne * sizeof(uint32_t) + (ne / 2 + 1) * sizeof(uint2));
     if (ne <= kKeygenFastMaxErrors && c->d_jump && !serial && lds <= kLdsBytesMax) {
         hipLaunchKernelGGL(keygen_fast_kernel, dim3((unsigned)((n_frames + kKeygenFrames - 1) / kKeygenFrames)),
                            dim3(kKeygenBlock), lds, stream, seeds, offset, (uint32_t)c->n, words, (uint32_t)ne,
-                           c->keygen_chunk, (uint32_t)n_frames, c->d_jump, ws->alice_w, ws->bob_w, exact_q, replay);
+                           c->keygen_chunk, (uint32_t)n_frames, c->d_jump, matrix ? nullptr : c->d_jpoly,
+                           ws->alice_w, ws->bob_w, exact_q, replay);
     } else {
         hipLaunchKernelGGL(keygen_kernel, dim3(blocks_for(n_frames, 64)), dim3(64), 0, stream, seeds, offset,
                            (uint32_t)n_frames, (uint32_t)c->n, words, (uint32_t)ne, ws->alice_w, ws->bob_w,
@@ -1918,10 +1989,7 @@ qkd_status qkd_counters_batch(const uint32_t* iterations, const uint8_t* syndrom
     qkd_status s = check_frames(n_frames);
     if (s != QKD_OK) return s;
     DeviceGuard g(device);
-    hipLaunchKernelGGL(counters_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counters);
-    hipLaunchKernelGGL(counters_kernel, dim3(blocks_for(n_frames, 256)), dim3(256), 0, (hipStream_t)stream,
-                       iterations, syndromes_match, keys_match, (uint32_t)n_frames, counters);
-    QKD_HIP(hipGetLastError());
+    QKD_HIP(launch_counters(iterations, syndromes_match, keys_match, n_frames, counters, (hipStream_t)stream));
     return QKD_OK;
 }
 
@@ -1948,13 +2016,8 @@ qkd_status qkd_trials_batch(const qkd_code* c, qkd_workspace* ws, const uint64_t
     s = decode_keys(c, ws, n_frames, q, max_iterations, msg_threshold, flags, nullptr, iterations,
                     syndromes_match, keys_match, (hipStream_t)stream);
     if (s != QKD_OK) return s;
-    if (counters) {
-        hipLaunchKernelGGL(counters_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counters);
-        hipLaunchKernelGGL(counters_kernel, dim3(blocks_for(n_frames, 256)), dim3(256), 0,
-                           (hipStream_t)stream, iterations, syndromes_match, keys_match,
-                           (uint32_t)n_frames, counters);
-        QKD_HIP(hipGetLastError());
-    }
+    if (counters) QKD_HIP(launch_counters(iterations, syndromes_match, keys_match, n_frames, counters,
+                                          (hipStream_t)stream));
     return QKD_OK;
 }
 

@@ -227,7 +227,7 @@ __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan,
         const qkds::f2 pv = RuleMath<kRuleSp32>::pair(xn, S);
         const uint32_t j = pw_chk(wt);
         const uint32_t neg = ((tsyn[j >> 5] >> (j & 31)) & 1u) ^
-                             (uint32_t)(DC <= 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^
+                             (uint32_t)(DC < 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^
                              (neg_t ? 1u : 0u);
         // pv.y >= +0 is never NaN (the sum enters through fminf), so clamp_msg
         // of +-pv.y is +-med3(pv.y, 0, thr) (thr > 0: check_decode_params)
@@ -389,7 +389,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         const uint32_t j = pw_chk(w);
         const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
         const uint32_t sigma =
-            sj ^ (uint32_t)(DC <= 32 ? seg_parity32(sgn, w) : seg_parity(sgn, w)) ^ (neg ? 1u : 0u);
+            sj ^ (uint32_t)(DC < 32 ? seg_parity32(sgn, w) : seg_parity(sgn, w)) ^ (neg ? 1u : 0u);
         return qkds::pack_iv(sigma ? -m.yx : m);
     };
     uint2 wa = pl[t * 64];
@@ -493,7 +493,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         const uint32_t j = pw_chk(wt);
         const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
         const uint32_t sigma =
-            sj ^ (uint32_t)(DC <= 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^ (neg_t ? 1u : 0u);
+            sj ^ (uint32_t)(DC < 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^ (neg_t ? 1u : 0u);
         ms.st(slot(wt), qkds::pack_iv(sigma ? -m.yx : m));
         // the next task's input bounds into the row
         row[lane] = qkds::pack_iv(ok_n ? ph_n : f2{0.0f, 0.0f});
@@ -767,7 +767,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     const bool dv3 = c.min_dv == kDvUnroll && c.max_dv == kDvUnroll;
     const bool tab2_on = fold1 && a.tab2_entries;
     uint32_t rnd = 0;    // rounds (iterations of any frame) run by this workgroup
-    if (tid == 0) { ctl[2] = 0; ctl[3] = 0; ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; }
+    if (tid == 0) { ctl[2] = 0; ctl[3] = 0; ctl[4] = 0; ctl[5] = 0; ctl[6] = 1; ctl[7] = 0; }
     static_assert(!SPEC || (RULE == kRuleSp64 && CLAMP), "speculation: binary64 rule, clamped messages");
     constexpr bool CKPT = SPEC == 2;
     static_assert(!CKPT || MODE == kModeKeys, "checkpointed speculation: keys path");
@@ -827,8 +827,12 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
         //      product rows are free until the first check phase) and its
         //      syndrome words from frame_syn_kernel.
         const uint64_t* bw = reinterpret_cast<const uint64_t*>(smem + L.tval);
+        // (keys path: this thread's word of Alice's key, for the key compare at
+        // the frame's end, arrays_equal :433; words <= kDecodeBlock)
+        uint64_t alice_word = 0;
         if (MODE == kModeKeys) {
             uint64_t* w = reinterpret_cast<uint64_t*>(smem + L.tval);
+            if (a.key_ok && tid < (int)a.words) alice_word = a.alice_w[(size_t)f * a.words + tid];
             for (int q = tid; q < (int)a.words; q += kDecodeBlock) w[q] = a.bob_w[(size_t)f * a.words + q];
             const uint32_t* sy = a.synw + (size_t)f * 2 * m_words;
             for (int q = tid; q < m_words; q += kDecodeBlock) {
@@ -921,8 +925,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     // (iteration 2 after the folded first one: the slots hold
                     // the phi bounds of exact b2c, psi_of_exact)
                     if (!folded && fold1 && it == 1) {
-                        spec_check_phase_psi<DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
-                                                   a.thr_up, rw, wave, lane);
+                        spec_check_phase_psi<DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n,
+                                                 a.thr_dn, a.thr_up, rw, wave, lane);
                         __syncthreads();
                     } else if (!folded) {
                         spec_check_phase_paired<DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
@@ -1165,7 +1169,27 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
         // ---- outputs: SP_result and the last hard decision (keys path:
         //      packed, for key_match_kernel's arrays_equal, :433)
         if (MODE == kModeKeys) {
-            for (int q = tid; q < (int)a.words; q += kDecodeBlock) a.zout[(size_t)f * a.words + q] = zw[q];
+            // keys_match = arrays_equal(alice, decoded) (:433, :96-106), fused
+            // here: this thread's word of the last hard decision against Alice's
+            // (block-wide OR through ctl[7], no static LDS: the dynamic
+            // allocation may take the whole 160 KB)
+            if (a.key_ok) {
+                bool mis = false;
+                if (tid < (int)a.words) {
+                    uint64_t d = zw[tid] ^ alice_word;
+                    if ((tid + 1) * 64 > c.n) d &= (1ull << (c.n - tid * 64)) - 1ull;
+                    mis = d != 0;
+                }
+                if (__any(mis) && lane == 0) atomicOr(ctl + 7, 1u);
+                __syncthreads();
+                if (tid == 0) {
+                    a.key_ok[f] = ctl[7] ? 0 : 1;
+                    ctl[7] = 0;
+                }
+            }
+            // the packed decision for bits_out (zout_unpack_kernel)
+            if (a.bits_out)
+                for (int q = tid; q < (int)a.words; q += kDecodeBlock) a.zout[(size_t)f * a.words + q] = zw[q];
         } else if (a.bits_out) {
             for (int i = tid; i < c.n; i += kDecodeBlock)
                 a.bits_out[(size_t)f * c.n + i] = (uint8_t)((zw[i >> 6] >> (i & 63)) & 1u);
@@ -1255,22 +1279,6 @@ __global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, cons
     }
 }
 
-// key_match_kernel: keys_match = arrays_equal(alice, decoded) (:433, :96-106),
-// one wave per frame over the packed words.
-__global__ __launch_bounds__(64) void key_match_kernel(const uint64_t* __restrict__ zout,
-                                                       const uint64_t* __restrict__ alice_w, uint32_t n,
-                                                       uint32_t words, uint8_t* key_ok) {
-    const uint32_t f = blockIdx.x;
-    bool mis = false;
-    for (uint32_t q = threadIdx.x; q < words; q += 64) {
-        uint64_t d = zout[(size_t)f * words + q] ^ alice_w[(size_t)f * words + q];
-        if ((q + 1) * 64 > n) d &= (1ull << (n - q * 64)) - 1ull;
-        mis |= d != 0;
-    }
-    const bool any = __any(mis);
-    if (threadIdx.x == 0) key_ok[f] = any ? 0 : 1;
-}
-
 __global__ void zout_unpack_kernel(const uint64_t* zout, uint32_t n, uint32_t words, uint32_t n_frames,
                                    uint8_t* out) {
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1290,9 +1298,7 @@ hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_key_match(const DecodeArgs& a, hipStream_t stream) {
-    if (a.key_ok)
-        hipLaunchKernelGGL(key_match_kernel, dim3(a.n_frames), dim3(64), 0, stream, a.zout, a.alice_w,
-                           (uint32_t)a.code.n, a.words, a.key_ok);
+    // (decode_split_kernel compares the keys itself: keys_match needs no launch)
     if (a.bits_out) {
         const size_t total = (size_t)a.n_frames * a.code.n;
         hipLaunchKernelGGL(zout_unpack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, a.zout,

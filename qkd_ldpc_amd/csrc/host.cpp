@@ -54,6 +54,8 @@ static void free_device(qkd_code* c) {
     c->d_plan_slot = nullptr;
     if (c->d_jump) (void)hipFree(c->d_jump);
     c->d_jump = nullptr;
+    if (c->d_jpoly) (void)hipFree(c->d_jpoly);
+    c->d_jpoly = nullptr;
     c->d_chk_bits = nullptr;
     c->d_chk_deg = nullptr;
     c->d_bit_chk = nullptr;
@@ -233,6 +235,13 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     qkdr::xoshiro_jump_matrices(c->keygen_chunk, kKeygenLevels, jump.data());
     QKD_HIP(hipMalloc(&c->d_jump, jump.size() * sizeof(uint64_t)));
     QKD_HIP(hipMemcpy(c->d_jump, jump.data(), jump.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    // the same jumps as polynomials, one per lane: x^(l * chunk) mod P (the
+    // default form, qkd_rng.h jump_poly_apply)
+    std::vector<uint64_t> jp((size_t)kKeygenLanes * 4);
+    if (!qkdr::xoshiro_jump_polys(c->keygen_chunk, kKeygenLanes, jp.data()))
+        return set_error(QKD_ERR_DEVICE, "xoshiro256 characteristic polynomial: unexpected degree");
+    QKD_HIP(hipMalloc(&c->d_jpoly, jp.size() * sizeof(uint64_t)));
+    QKD_HIP(hipMemcpy(c->d_jpoly, jp.data(), jp.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
     return QKD_OK;
 }
 

@@ -241,11 +241,13 @@ __device__ __forceinline__ int seg_parity(uint64_t ballot, uint2 w) {
     // (<= 64) of them, count
     const uint64_t sh = ballot >> pw_start(w);
     const int deg = pw_deg(w);
-    if (deg <= 32) return __popc(__builtin_amdgcn_ubfe((uint32_t)sh, 0, (uint32_t)deg)) & 1;
+    // (v_bfe_u32 takes its width from 5 bits: a width of 32 would read as 0)
+    if (deg < 32) return __popc(__builtin_amdgcn_ubfe((uint32_t)sh, 0, (uint32_t)deg)) & 1;
     const uint64_t m = deg == 64 ? ~0ull : ((1ull << deg) - 1ull);
     return __popcll(sh & m) & 1;
 }
-// The same for segments known to be at most 32 lanes long.
+// The same for segments known to be shorter than 32 lanes (check-degree
+// buckets up to 16; v_bfe_u32's width field has 5 bits).
 __device__ __forceinline__ int seg_parity32(uint64_t ballot, uint2 w) {
     const uint32_t sh = (uint32_t)(ballot >> pw_start(w));
     return __popc(__builtin_amdgcn_ubfe(sh, 0, (uint32_t)pw_deg(w))) & 1;

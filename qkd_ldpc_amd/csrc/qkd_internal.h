@@ -150,6 +150,8 @@ struct qkd_code {
     // d_jump[b] = T^(chunk * 2^b)
     uint32_t keygen_chunk = 0;
     uint64_t* d_jump = nullptr;
+    // the same jumps as polynomials: d_jpoly[l] = x^(l * chunk) mod P (4 words)
+    uint64_t* d_jpoly = nullptr;
     int cu_count = 0;
     qkd_workspace* default_ws = nullptr;
 

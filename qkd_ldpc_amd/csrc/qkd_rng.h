@@ -213,6 +213,128 @@ inline void xoshiro_jump_matrices(uint64_t chunk, int levels, uint64_t* out) {
     delete[] tmp;
 }
 
+// ---------------------------------------------------------------------------
+// Jump-ahead by polynomial (the default of keygen_fast_kernel).
+//
+// T satisfies its characteristic polynomial P (degree 256; xoshiro256's is
+// primitive), so T^k = (x^k mod P)(T): with p = x^k mod P = sum_i p_i x^i,
+//   T^k s = sum_{i < 256} p_i T^i s,
+// i.e. 256 state steps from s, XOR-accumulating the states whose coefficient
+// is set: about 256 x (one state step + a masked 256-bit XOR) operations per
+// lane, no matrix reads (the matrix form above costs 256 masked column XORs
+// per jump level, with the columns streamed from memory). This is the
+// construction of the generator's own published jump() (its JUMP constant is
+// x^(2^128) mod P; tests/native/jump_check.cpp checks that too).
+// A polynomial of degree < 256 is 4 words, bit i = coefficient of x^i; P
+// itself needs bit 256 (implicit: P = x^256 + the 4 words).
+// ---------------------------------------------------------------------------
+
+// P by Berlekamp-Massey over GF(2) on 512 output bits of a linear functional
+// of the state (bit 0 of s0 after each step, from a nonzero state): the
+// sequence's connection polynomial C(x) = 1 + c_1 x + ... + c_L x^L has
+// L = 256 for a primitive T, and P(x) = x^L C(1/x). Returns false if L != 256.
+inline bool xoshiro_charpoly(uint64_t P[4]) {
+    const int n = 512;
+    uint8_t seq[512];
+    uint64_t s[4] = {0x9e3779b97f4a7c15ull, 0x0123456789abcdefull, 0xfedcba9876543210ull, 1ull};
+    for (int i = 0; i < n; ++i) {
+        seq[i] = (uint8_t)(s[0] & 1u);
+        xoshiro_step_state(s);
+    }
+    uint8_t C[513] = {0}, B[513] = {0}, Tm[513];
+    C[0] = B[0] = 1;
+    int L = 0, m = 1;
+    for (int i = 0; i < n; ++i) {
+        uint8_t d = seq[i];
+        for (int j = 1; j <= L; ++j) d ^= (uint8_t)(C[j] & seq[i - j]);
+        if (!d) {
+            ++m;
+            continue;
+        }
+        for (int j = 0; j <= n; ++j) Tm[j] = C[j];
+        for (int j = 0; j + m <= n; ++j) C[j + m] ^= B[j];
+        if (2 * L <= i) {
+            L = i + 1 - L;
+            for (int j = 0; j <= n; ++j) B[j] = Tm[j];
+            m = 1;
+        } else {
+            ++m;
+        }
+    }
+    if (L != 256) return false;
+    P[0] = P[1] = P[2] = P[3] = 0;
+    for (int i = 0; i < 256; ++i)              // coefficient of x^i in P is c_{256 - i}
+        if (C[256 - i]) P[i >> 6] |= 1ull << (i & 63);
+    return true;
+}
+
+// r <- r * x mod P
+inline void poly_mulx_mod(uint64_t r[4], const uint64_t P[4]) {
+    const uint64_t top = r[3] >> 63;
+    r[3] = (r[3] << 1) | (r[2] >> 63);
+    r[2] = (r[2] << 1) | (r[1] >> 63);
+    r[1] = (r[1] << 1) | (r[0] >> 63);
+    r[0] <<= 1;
+    if (top) {
+        r[0] ^= P[0];
+        r[1] ^= P[1];
+        r[2] ^= P[2];
+        r[3] ^= P[3];
+    }
+}
+
+// r <- a * b mod P (carry-less, shift-and-add over b's bits)
+inline void poly_mulmod(const uint64_t a[4], const uint64_t b[4], const uint64_t P[4], uint64_t r[4]) {
+    uint64_t acc[4] = {0, 0, 0, 0}, t[4] = {a[0], a[1], a[2], a[3]};
+    for (int i = 0; i < 256; ++i) {
+        if ((b[i >> 6] >> (i & 63)) & 1u)
+            for (int w = 0; w < 4; ++w) acc[w] ^= t[w];
+        poly_mulx_mod(t, P);
+    }
+    for (int w = 0; w < 4; ++w) r[w] = acc[w];
+}
+
+// out[l] = x^(l * chunk) mod P for lanes l = 0 .. lanes-1 (4 words each).
+inline bool xoshiro_jump_polys(uint64_t chunk, int lanes, uint64_t* out) {
+    uint64_t P[4];
+    if (!xoshiro_charpoly(P)) return false;
+    uint64_t step[4] = {1, 0, 0, 0};                 // x^chunk mod P
+    for (uint64_t k = 0; k < chunk; ++k) poly_mulx_mod(step, P);
+    uint64_t r[4] = {1, 0, 0, 0};
+    for (int l = 0; l < lanes; ++l) {
+        for (int w = 0; w < 4; ++w) out[(size_t)l * 4 + w] = r[w];
+        uint64_t nr[4];
+        poly_mulmod(r, step, P, nr);
+        for (int w = 0; w < 4; ++w) r[w] = nr[w];
+    }
+    return true;
+}
+
+// s <- p(T) s for a jump polynomial p (4 words): 256 state steps, the states
+// of the set coefficients XOR-accumulated (masks, no branches).
+QKD_RHD void jump_poly_apply(const uint64_t p[4], uint64_t s[4]) {
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint64_t t[4] = {s[0], s[1], s[2], s[3]};
+    for (int w = 0; w < 4; ++w) {
+        const uint64_t pw = p[w];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 8
+#endif
+        for (int j = 0; j < 64; ++j) {
+            const uint64_t m = (uint64_t)0 - ((pw >> j) & 1u);
+            a0 ^= t[0] & m;
+            a1 ^= t[1] & m;
+            a2 ^= t[2] & m;
+            a3 ^= t[3] & m;
+            xoshiro_step_state(t);
+        }
+    }
+    s[0] = a0;
+    s[1] = a1;
+    s[2] = a2;
+    s[3] = a3;
+}
+
 // Draw count of one trial: N alice bits, the lone swap draw (even N), one
 // Lemire draw per shuffle pair (std::shuffle, see shuffle_low_positions),
 // without rejections.

@@ -24,6 +24,38 @@ int main() {
             }
         }
     }
+    // the polynomial form (the default of keygen_fast_kernel): lane l jumps
+    // by x^(l * chunk) mod P; the same states as stepping
+    for (uint64_t chunk : {1ull, 64ull, 192ull, 256ull, 1000ull}) {
+        std::vector<uint64_t> polys(64 * 4);
+        if (!qkdr::xoshiro_jump_polys(chunk, 64, polys.data())) bad += 1000;
+        for (uint64_t seed : {0ull, 5ull, 777ull, 0x1cac6d74bb9d6789ull}) {
+            qkdr::Xoshiro256pp h;
+            h.seed(seed);
+            for (int lane = 0; lane < 64; ++lane) {
+                qkdr::Xoshiro256pp g;
+                g.seed(seed);
+                uint64_t s[4] = {g.s0, g.s1, g.s2, g.s3};
+                qkdr::jump_poly_apply(polys.data() + (size_t)lane * 4, s);
+                if (s[0] != h.s0 || s[1] != h.s1 || s[2] != h.s2 || s[3] != h.s3) bad++;
+                for (uint64_t k = 0; k < chunk; ++k) h.next();
+            }
+        }
+    }
+    // the generator's published jump(): JUMP = x^(2^128) mod P
+    {
+        uint64_t P[4], r[4] = {2, 0, 0, 0};          // x
+        if (!qkdr::xoshiro_charpoly(P)) bad += 1000;
+        for (int k = 0; k < 128; ++k) {              // square 128 times: x^(2^128)
+            uint64_t t[4];
+            qkdr::poly_mulmod(r, r, P, t);
+            for (int w = 0; w < 4; ++w) r[w] = t[w];
+        }
+        const uint64_t JUMP[4] = {0x180ec6d33cfd0abaull, 0xd5a61266f0c9392cull, 0xa9582618e03fc9aaull,
+                                  0x39abdc4529b1661cull};
+        for (int w = 0; w < 4; ++w)
+            if (r[w] != JUMP[w]) bad += 100;
+    }
     std::printf("%ld\n", bad);
     return 0;
 }

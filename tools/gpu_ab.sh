@@ -1,0 +1,27 @@
+# A/B of experimental library builds (exp_libs/<name>/, tools/ab_build.sh)
+# against the in-tree one on one GPU: a parity subset per build, then the
+# headline bench alternating builds for REPS rounds (decoder-kernel and step
+# times). Every GPU step has its own time limit; a failure ends the script.
+set -u
+cd "$(dirname "$0")/.."
+O=gpurun_out/ab
+mkdir -p $O
+export TMPDIR=/tmp
+REPS=${REPS:-3}
+LIBS="base ${LIBS:-$(ls exp_libs)}"
+libpath() { [ "$1" = base ] && echo qkd_ldpc_amd/lib/libqkd_ldpc_amd.so || echo exp_libs/$1/libqkd_ldpc_amd.so; }
+for l in $LIBS; do
+  QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=$(libpath $l) timeout -k 10 300 python -u -m pytest tests/test_spec.py -q -x \
+    --timeout 120 --timeout-method thread -k "${PARITY_K:-config2_every_cap or bits_match_oracle}" > $O/parity_$l.log 2>&1
+  rc=$?; echo "$l parity rc=$rc $(tail -n 1 $O/parity_$l.log)"
+  [ $rc -eq 0 ] || exit $rc
+done
+for r in $(seq $REPS); do
+  for l in $LIBS; do
+    QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=$(libpath $l) timeout -k 10 120 python bench.py --no-cpu-baseline --no-variants \
+      --no-sweeps --steps 20 ${BENCH_EXTRA:-} > $O/bench_$l.json 2> $O/bench_$l.err || { tail $O/bench_$l.err; exit 1; }
+    python -c "
+import json;d=json.loads(open('$O/bench_$l.json').read().strip().splitlines()[-1])
+print('$l', 'step', round(d['ms_per_step'],4), 'kernel', round(d['roofline']['kernel_ms'],4), 'call', round(d['roofline']['call_ms'],4), 'e2e', round(d['end_to_end']['ms_per_step'],4) if 'end_to_end' in d else '', 'replays', d['speculation']['replayed_frames'])"
+  done
+done
