@@ -246,7 +246,8 @@ def config3_sweep(args, H, Q, dev):
                        "sum_iterations": st["sum_iters_sp"],
                        "reference": {"qber_actual": rp["qber_actual"], "fer": rp["fer"], "mean_it": rp["mean_it"]},
                        "matches_reference": bool(abs(st["fer"] - rp["fer"]) < 1e-12 and
-                                                 abs(st["iterations_successful_sp_mean"] - rp["mean_it"]) <= 5e-4)})
+                                                 abs(st["iterations_successful_sp_mean"] - rp["mean_it"])
+                                                 <= 5e-4 + 1e-9)})
     ws.close()
     return {"what": "configs[2]: 8 QBER points x 10,000 trials, qkd_trials_batch per point (keygen + decode + "
                     "counters), fresh workspace, ascending points", "total_s": total,
@@ -394,15 +395,13 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     decoder_ms(L, ws, True)      # HIP events around each decoder launch, on its stream
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -412,6 +411,12 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # the whole library call (pack, frame syndromes, decoder), HIP events around it,
+    # in a short untimed pass after the timed region
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for k in range(5):
+        step(evs[k])
+    torch.cuda.synchronize()
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
 
     c = Q.read_counters(counters)
@@ -459,7 +464,7 @@ def main():
                 "qkd_qkd_ldpc_batch: pack + frame_syn_kernel + decoder + key_match_kernel"),
             "speculation": {
                 "replayed_frames": replays,
-                "frames": F * (args.steps + args.warmup),
+                "frames": F * (args.steps + args.warmup + 5),
                 "note": "frames whose interval iterations could not certify every hard "
                         "decision, decoded again exactly (outputs bit-exact either way)",
             },

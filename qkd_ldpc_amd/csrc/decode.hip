@@ -622,26 +622,41 @@ __global__ void syndrome_kernel(DeviceCode c, const uint8_t* bits, uint32_t n_fr
 // byte array is the uint64 word array); bits past n are 0. 8-byte loads when
 // every frame row is 8-byte aligned (n % 8 == 0), byte loads otherwise.
 __global__ void pack_kernel(const uint8_t* bytes0, const uint8_t* bytes1, uint32_t n, uint32_t words,
-                            uint32_t n_frames, uint64_t* out0, uint64_t* out1) {
+                            uint32_t n_frames, uint64_t* out0, uint64_t* out1, uint32_t wide) {
+    // wide (the host's choice: n % 32 == 0 and both arrays 16-byte aligned): 32
+    // key bytes -> 4 packed bytes per thread (two 16-byte loads); else one
+    // packed byte per thread
     const uint8_t* bytes = blockIdx.y ? bytes1 : bytes0;
     uint64_t* out = blockIdx.y ? out1 : out0;
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t per_frame = (size_t)words * 8;
+    if (wide) {
+        const size_t per4 = per_frame / 4;            // 4-byte output groups per frame
+        if (gid >= (size_t)n_frames * per4) return;
+        const size_t f = gid / per4;
+        const uint32_t b = (uint32_t)(gid - f * per4);   // output bytes 4b .. 4b+3
+        uint32_t m = 0;
+        if ((size_t)b * 32 < n) {
+            const uint4* src = reinterpret_cast<const uint4*>(bytes + f * n + (size_t)b * 32);
+            const uint4 v0 = src[0], v1 = src[1];
+            const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t t = w[k] & 0x01010101u;            // byte q's LSB at bit 8q
+                m |= ((t * 0x01020408u) >> 24 & 0xfu) << (4 * k); // byte q -> bit 24 + q
+            }
+        }
+        reinterpret_cast<uint32_t*>(out)[gid] = m;
+        return;
+    }
     if (gid >= (size_t)n_frames * per_frame) return;
     const size_t f = gid / per_frame;
     const uint32_t b = (uint32_t)(gid - f * per_frame);
     const uint8_t* src = bytes + f * n;
     uint32_t m = 0;
-    if ((n & 7u) == 0) {
-        if (b * 8 < n) {
-            const uint64_t v = *reinterpret_cast<const uint64_t*>(src + (size_t)b * 8) & 0x0101010101010101ull;
-            m = (uint32_t)((v * 0x0102040810204080ull) >> 56);   // byte k's LSB -> bit k
-        }
-    } else {
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t i = b * 8 + k;
-            if (i < n) m |= (uint32_t)(src[i] & 1u) << k;
-        }
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t i = b * 8 + k;
+        if (i < n) m |= (uint32_t)(src[i] & 1u) << k;
     }
     reinterpret_cast<uint8_t*>(out)[gid] = (uint8_t)m;
 }
@@ -894,12 +909,23 @@ __global__ __launch_bounds__(1024) void counters_one_kernel(const uint32_t* iter
             mx = max(mx, (uint32_t)it);
         }
     }
-    atomicAdd(&s_sum[1], c1);
-    atomicAdd(&s_sum[2], c2);
-    atomicAdd(&s_sum[3], c3);
-    atomicAdd(&s_sum[4], c4);
-    atomicMin(&s_min, mn);
-    atomicMax(&s_max, mx);
+    // wave reductions first: one LDS atomic per wave and quantity
+    for (int o = 32; o > 0; o >>= 1) {
+        c1 += __shfl_xor(c1, o);
+        c2 += __shfl_xor(c2, o);
+        c3 += __shfl_xor(c3, o);
+        c4 += __shfl_xor(c4, o);
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&s_sum[1], c1);
+        atomicAdd(&s_sum[2], c2);
+        atomicAdd(&s_sum[3], c3);
+        atomicAdd(&s_sum[4], c4);
+        atomicMin(&s_min, mn);
+        atomicMax(&s_max, mx);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         out->frames = n_frames;
@@ -1212,7 +1238,9 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             a.c2b_stride = ((slots - L.S + 31) & ~(size_t)31) + pad;
             a.lds_budget = (uint32_t)budget;
             a.counter = ws->counter;
-            QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));     // [0] frame queue, [1] replays
+            // [0] frame queue, [1] replays: zeroed by frame_syn_kernel on the
+            // keys path (it runs first on this stream), by a memset otherwise
+            if (mode != kModeKeys) QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));
             static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;
             a.phase = nullptr;
             if (timing) {
@@ -1449,8 +1477,10 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     // from a checkpoint instead, from that QBER up
     if (ws->spec_stat_pending && hipEventQuery(ws->spec_stat_ev) == hipSuccess) {
         ws->spec_stat_pending = false;
-        if ((double)*ws->spec_stat_host > kSpecCkptSwitch * (double)ws->spec_stat_frames)
-            ws->spec_ckpt_q = std::min(ws->spec_ckpt_q, ws->spec_stat_q);
+        const bool over = (double)*ws->spec_stat_host > kSpecCkptSwitch * (double)ws->spec_stat_frames;
+        if (over) ws->spec_ckpt_q = std::min(ws->spec_ckpt_q, ws->spec_stat_q);
+        int& cnt = ws->spec_clean[ws->spec_stat_q];
+        cnt = over ? 0 : cnt + 1;
     }
     // at and above that QBER: the checkpointed speculation (QKD_CKPT_UNSAT
     // overrides its trigger; 0: exact iterations only)
@@ -1467,6 +1497,13 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     }
     qkd_status st = launch_decode(c, ws, a, kModeKeys, flags, stream);
     if (st != QKD_OK || a.spec_cap == 0 || a.ckpt_unsat || ws->spec_stat_pending) return st;
+    // (a QBER whose last two samples stayed under the switch is sampled again
+    // only every kSpecStatEvery calls: each sample is a device-to-host copy
+    // and an event on the caller's stream)
+    {
+        auto& cnt = ws->spec_clean[q];
+        if (cnt >= 2 && (++ws->spec_skip % kSpecStatEvery) != 0) return st;
+    }
     if (!ws->spec_stat_host) {
         if (hipHostMalloc(reinterpret_cast<void**>(&ws->spec_stat_host), 8, hipHostMallocDefault) != hipSuccess ||
             hipEventCreateWithFlags(&ws->spec_stat_ev, hipEventDisableTiming) != hipSuccess)
@@ -1501,9 +1538,12 @@ qkd_status qkd_qkd_ldpc_batch(const qkd_code* c, qkd_workspace* ws, const uint8_
     if (s != QKD_OK) return s;
     const uint32_t words = (uint32_t)((c->n + 63) / 64);
     const size_t nw = n_frames * words;
-    // Alice's and Bob's keys in one launch (grid.y selects the key)
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(nw * 8, 256), 2), dim3(256), 0, (hipStream_t)stream, alice, bob,
-                       (uint32_t)c->n, words, (uint32_t)n_frames, ws->alice_w, ws->bob_w);
+    // Alice's and Bob's keys in one launch (grid.y selects the key; the wide
+    // form needs both arrays 16-byte aligned)
+    const bool wide = (c->n % 32) == 0 && ((reinterpret_cast<uintptr_t>(alice) | reinterpret_cast<uintptr_t>(bob)) & 15u) == 0;
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(wide ? nw * 2 : nw * 8, 256), 2), dim3(256), 0, (hipStream_t)stream,
+                       alice, bob, (uint32_t)c->n, words, (uint32_t)n_frames, ws->alice_w, ws->bob_w,
+                       wide ? 1u : 0u);
     QKD_HIP(hipGetLastError());
     return decode_keys(c, ws, n_frames, qber, max_iterations, msg_threshold, flags, bits_out, iterations,
                        syndromes_match, keys_match, (hipStream_t)stream);

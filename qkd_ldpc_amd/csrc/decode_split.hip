@@ -1219,10 +1219,14 @@ constexpr int kSynBlock = 256;
 constexpr int kSynRow = 8;
 __global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, const uint64_t* __restrict__ alice_w,
                                                               const uint64_t* __restrict__ bob_w, uint32_t words,
-                                                              uint32_t n_frames, uint32_t lsign, uint32_t* synw) {
+                                                              uint32_t n_frames, uint32_t lsign, uint32_t* synw,
+                                                              uint32_t* counter) {
     // [kSynFrames][2 * words] pairs (Alice's 32-bit word, Bob's 32-bit word):
     // one 8-byte LDS read gives both keys' bit
     extern __shared__ uint2 kw[];
+    // the decoder's frame queue and replay count (decode.hip launch_decode:
+    // this kernel runs first on the stream, in place of a memset)
+    if (blockIdx.x == 0 && threadIdx.x < 2) counter[threadIdx.x] = 0;
     const uint32_t w32 = 2 * words;
     const uint32_t f0 = blockIdx.x * kSynFrames;
     const uint32_t nf = min((uint32_t)kSynFrames, n_frames - f0);
@@ -1293,7 +1297,7 @@ hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
     const size_t lds = (size_t)kSynFrames * 2 * a.words * sizeof(uint64_t);
     hipLaunchKernelGGL(frame_syn_kernel, dim3((a.n_frames + kSynFrames - 1) / kSynFrames), dim3(kSynBlock), lds,
                        stream, a.code, a.alice_w, a.bob_w, a.words, a.n_frames, lsign,
-                       const_cast<uint32_t*>(a.synw));
+                       const_cast<uint32_t*>(a.synw), a.counter);
     return hipGetLastError();
 }
 

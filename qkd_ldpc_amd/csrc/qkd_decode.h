@@ -23,6 +23,9 @@ constexpr double kSpecCkptSwitch = 1.0 / 16.0;
 // Replay fraction above which speculation stops: within a launch for the
 // frames still to start (decode_split.hip), across calls for that QBER and up.
 constexpr double kSpecReplayMax = 1.0 / 6.0;
+// decode_keys samples the replay count of a QBER that twice stayed under
+// kSpecCkptSwitch only once every this many calls
+constexpr uint64_t kSpecStatEvery = 64;
 
 // Largest check degree the first-iteration table covers.
 constexpr int kFirstTableDeg = 16;

@@ -4,6 +4,7 @@
 
 #include <cstdarg>
 #include <cstdint>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -116,6 +117,10 @@ struct qkd_workspace {
     double spec_stat_q = 0.0;
     size_t spec_stat_frames = 0;
     double spec_ckpt_q = 2.0;
+    // per QBER: consecutive samples under the switch (decode_keys samples a
+    // QBER with two such samples only every kSpecStatEvery calls)
+    std::map<double, int> spec_clean;
+    uint64_t spec_skip = 0;
     // checkpointed speculation: one saved message store per resident workgroup
     double* ckpt = nullptr;
     size_t ckpt_slots = 0;

@@ -396,3 +396,21 @@ def test_irregular_high_degree_bits_keys_path(Q, oracle_mod, tmp_path):
         assert (r.iterations.cpu().numpy() == want["iters"]).all()
         assert (r.syndromes_match.cpu().numpy().astype(bool) == want["sp_ok"]).all()
         assert (r.keys_match.cpu().numpy().astype(bool) == want["key_ok"]).all()
+
+
+def test_qkd_ldpc_unaligned_key_bytes(Q, H, golden_vectors):
+    """Key bytes whose rows start off a 16-byte boundary take the packing kernel's
+    byte path (the wide path needs N % 32 == 0 and aligned arrays); same outputs."""
+    seeds = seeds_dev(Q.make_seeds(777, 64))
+    a, b, q = Q.keygen(H, seeds, 0.02)
+    buf_a = torch.zeros(64 * 10240 + 16, dtype=torch.uint8, device="cuda")
+    buf_b = torch.zeros(64 * 10240 + 16, dtype=torch.uint8, device="cuda")
+    ua = buf_a[3:3 + 64 * 10240].view(64, 10240)
+    ub = buf_b[5:5 + 64 * 10240].view(64, 10240)
+    ua.copy_(a)
+    ub.copy_(b)
+    r = Q.qkd_ldpc(H, ua, ub, float(q[0]), 50, 100.0, True, want_bits=True)
+    torch.cuda.synchronize()
+    assert (r.iterations.cpu().numpy() == golden_vectors["c2_iters"][:64]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c2_ko"][:64]).all()
+    assert (r.bits.cpu().numpy() == a.cpu().numpy()).all()
