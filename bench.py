@@ -68,6 +68,8 @@ def parse():
                     help="decoder rule of the headline line (sp_f64 = the reference's)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the side measurement of the binary32 variants")
+    ap.add_argument("--kernel-events", choices=["on", "off"], default="on",
+                    help="HIP events around each decoder launch inside the timed loop (off: diagnostics)")
     ap.add_argument("--no-sweeps", action="store_true",
                     help="skip the config-3 QBER sweep and the config-4 rank-share lines")
     return ap.parse_args()
@@ -398,7 +400,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    decoder_ms(L, ws, True)      # HIP events around each decoder launch, on its stream
+    if args.kernel_events == "on":
+        decoder_ms(L, ws, True)      # HIP events around each decoder launch, on its stream
     t0 = time.perf_counter()
     for k in range(args.steps):
         step()
@@ -406,7 +409,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    dec_ms = decoder_ms(L, ws, False)
+    if args.kernel_events == "on":
+        dec_ms = decoder_ms(L, ws, False)
+    else:
+        decoder_ms(L, ws, True)
+        for k in range(3):
+            step()
+        dec_ms = decoder_ms(L, ws, False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -392,6 +392,32 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
             sj ^ (uint32_t)(DC < 32 ? seg_parity32(sgn, w) : seg_parity(sgn, w)) ^ (neg ? 1u : 0u);
         return qkds::pack_iv(sigma ? -m.yx : m);
     };
+#ifndef QKD_PSI_LA
+#define QKD_PSI_LA 1
+#endif
+    if constexpr (QKD_PSI_LA >= 2) {
+        // slots two tasks ahead, plan words three (the global slots' L2
+        // latency under the kernel's own store traffic)
+        uint2 w0 = pl[t * 64], w1 = pl[(t + NW) * 64], w2 = pl[(t + 2 * NW) * 64];
+        double x0 = ms.ld(slot(w0)), x1 = ms.ld(slot(w1));
+        uint32_t pend = 0xffffffffu;
+        double pv = 0;
+        for (;;) {
+            const uint2 w3 = pl[(t + 3 * NW) * 64];
+            const double x2 = ms.ld(slot(w2));
+            if (pend != 0xffffffffu) ms.st(pend, pv);
+            pv = edge(x0, w0);
+            pend = slot(w0);
+            t += NW;
+            if (t >= n_tasks) break;
+            w0 = w1;
+            w1 = w2;
+            w2 = w3;
+            x0 = x1;
+            x1 = x2;
+        }
+        ms.st(pend, pv);
+    } else {
     uint2 wa = pl[t * 64];
     uint2 wb = pl[(t + NW) * 64];
     double xa = ms.ld(slot(wa));
@@ -416,6 +442,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         wa = wc;
     }
     ms.st(pend, pv);
+    }
     if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
 }
 
@@ -463,9 +490,22 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
     }
     uint64_t sgn_t = __ballot(neg_t);
     double xn = ms.ld(slot(wn));
+#ifndef QKD_PAIR_LA
+#define QKD_PAIR_LA 2
+#endif
+    // (QKD_PAIR_LA 3: slots three tasks ahead, plan words four)
+    uint2 w3 = pl[(t + 3 * NW) * 64];
+    double xnn = QKD_PAIR_LA >= 3 ? ms.ld(slot(wnn)) : 0.0;
     for (;;) {
-        const uint2 w3 = pl[(t + 3 * NW) * 64];
-        const double xnn = ms.ld(slot(wnn));
+        uint2 w4;
+        double x3;
+        if constexpr (QKD_PAIR_LA >= 3) {
+            w4 = pl[(t + 4 * NW) * 64];
+            x3 = ms.ld(slot(w3));
+        } else {
+            w3 = pl[(t + 3 * NW) * 64];
+            xnn = ms.ld(slot(wnn));
+        }
         bool neg_n;
         f2 ab_n;
         const bool ok_n = input(xn, wn, neg_n, ab_n);
@@ -505,6 +545,10 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         wn = wnn;
         wnn = w3;
         xn = xnn;
+        if constexpr (QKD_PAIR_LA >= 3) {
+            w3 = w4;
+            xnn = x3;
+        }
     }
     if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
 }
@@ -560,9 +604,11 @@ __device__ void fold_table_fill(const DeviceCode& c, const double* ctab, double 
 // in xunc (the syndrome test then decides whether the round can stand).
 // Needs DeviceCode::bit_code (bit degree <= 3, M <= 65536, check degree <= 16).
 #ifndef QKD_IV_CHUNK
-#define QKD_IV_CHUNK 3
+#define QKD_IV_CHUNK 2
 #endif
-constexpr int kIvChunk = QKD_IV_CHUNK;       // rounds per load batch
+// rounds per load batch (2: measured -1 % per config-2 batch against 3, the
+// registers go to the check phases)
+constexpr int kIvChunk = QKD_IV_CHUNK;
 // DV3: every bit has exactly kDvUnroll (3) checks (a column-weight-3 code,
 // like the reference's N = 10240 one): no per-degree guards, so the round is
 // straight-line code except one branch around the hard decision's syndrome
@@ -579,10 +625,9 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
     const uint32_t n_pad = (uint32_t)c.n_pad;
     const double llr_p = a.log_p;
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
-    for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kIvChunk) {
-        double v[kIvChunk][kDvUnroll];
-        uint64_t bc[kIvChunk];                 // the bits' packed words (DeviceCode::bit_code)
-        uint32_t pat[kIvChunk];                // FOLD with ftab: the bits' degree patterns
+    // one batch of kIvChunk rounds: its loads, then its rounds
+    typedef double VB[kIvChunk][kDvUnroll];
+    auto batch_load = [&](int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
 #pragma unroll
         for (int u = 0; u < kIvChunk; ++u) {
             const int i = tid + (r0 + u) * kDecodeBlock;
@@ -594,6 +639,8 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             for (int k = 0; k < kDvUnroll; ++k)
                 v[u][k] = FOLD ? 0.0 : ms.ld_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i);
         }
+    };
+    auto batch_compute = [&](int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
 #pragma unroll
         for (int u = 0; u < kIvChunk; ++u) {
             const int r = r0 + u;
@@ -700,6 +747,33 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 for (int k = 0; k < kDvUnroll; ++k)
                     if (k < deg) ms.st_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i, qkds::pack_iv(bo[k]));
             }
+        }
+    };
+#ifndef QKD_IV_PIPE
+#define QKD_IV_PIPE 0
+#endif
+    if constexpr (QKD_IV_PIPE && !FOLD) {
+        // software-pipelined: the next batch's loads are issued before this
+        // batch's rounds (two batches of registers)
+        VB va, vb;
+        uint64_t ba[kIvChunk], bb[kIvChunk];
+        uint32_t pa[kIvChunk], pb[kIvChunk];
+        batch_load(0, va, ba, pa);
+        for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += 2 * kIvChunk) {
+            const bool more = (r0 + kIvChunk) * kDecodeBlock < c.n;
+            if (more) batch_load(r0 + kIvChunk, vb, bb, pb);
+            batch_compute(r0, va, ba, pa);
+            if (!more) break;
+            if ((r0 + 2 * kIvChunk) * kDecodeBlock < c.n) batch_load(r0 + 2 * kIvChunk, va, ba, pa);
+            batch_compute(r0 + kIvChunk, vb, bb, pb);
+        }
+    } else {
+        for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kIvChunk) {
+            VB v;
+            uint64_t bc[kIvChunk];                 // the bits' packed words (DeviceCode::bit_code)
+            uint32_t pat[kIvChunk];                // FOLD with ftab: the bits' degree patterns
+            batch_load(r0, v, bc, pat);
+            batch_compute(r0, v, bc, pat);
         }
     }
 }
@@ -827,12 +901,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
         //      product rows are free until the first check phase) and its
         //      syndrome words from frame_syn_kernel.
         const uint64_t* bw = reinterpret_cast<const uint64_t*>(smem + L.tval);
-        // (keys path: this thread's word of Alice's key, for the key compare at
-        // the frame's end, arrays_equal :433; words <= kDecodeBlock)
-        uint64_t alice_word = 0;
         if (MODE == kModeKeys) {
             uint64_t* w = reinterpret_cast<uint64_t*>(smem + L.tval);
-            if (a.key_ok && tid < (int)a.words) alice_word = a.alice_w[(size_t)f * a.words + tid];
             for (int q = tid; q < (int)a.words; q += kDecodeBlock) w[q] = a.bob_w[(size_t)f * a.words + q];
             const uint32_t* sy = a.synw + (size_t)f * 2 * m_words;
             for (int q = tid; q < m_words; q += kDecodeBlock) {
@@ -1174,9 +1244,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // (block-wide OR through ctl[7], no static LDS: the dynamic
             // allocation may take the whole 160 KB)
             if (a.key_ok) {
+                // (Alice's word read here rather than held in registers
+                // through the frame's iterations)
                 bool mis = false;
                 if (tid < (int)a.words) {
-                    uint64_t d = zw[tid] ^ alice_word;
+                    uint64_t d = zw[tid] ^ a.alice_w[(size_t)f * a.words + tid];
                     if ((tid + 1) * 64 > c.n) d &= (1ull << (c.n - tid * 64)) - 1ull;
                     mis = d != 0;
                 }
@@ -1214,7 +1286,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
 // first-iteration product, q_j = s_j ^ (H * bob)_j ^ (deg_j & sign(log_p))
 // (first_check_phase), one bit per check in whole 64-check groups. kSynFrames
 // frames per workgroup share each load of a check's row.
-constexpr int kSynFrames = 4;
+#ifndef QKD_SYN_FRAMES
+#define QKD_SYN_FRAMES 4
+#endif
+constexpr int kSynFrames = QKD_SYN_FRAMES;
 constexpr int kSynBlock = 256;
 constexpr int kSynRow = 8;
 __global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, const uint64_t* __restrict__ alice_w,

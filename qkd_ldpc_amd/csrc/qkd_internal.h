@@ -14,7 +14,10 @@
 namespace qkd {
 
 // Threads per decode workgroup: one workgroup decodes one frame at a time.
-constexpr int kDecodeBlock = 1024;
+#ifndef QKD_DECODE_BLOCK
+#define QKD_DECODE_BLOCK 1024
+#endif
+constexpr int kDecodeBlock = QKD_DECODE_BLOCK;
 // Second-iteration tanh table (decode.hip): entries per degree pattern are
 // 2^(1 + max_dv) sign codes x max_dv rows; the table is used when
 // max_dv <= kTab2MaxDv and n_pat * entries <= kTab2MaxEntries.
@@ -30,7 +33,7 @@ constexpr int kMaxCheckDegree = 64;
 constexpr int kMaxBitsLds = 20480;
 // The split-store kernels (decode_split.hip): Bob's bits of a thread's
 // bit-phase rounds in one 64-bit register, 64 rounds of kDecodeBlock bits
-constexpr int kMaxBitsSplit = 64 * 1024;
+constexpr int kMaxBitsSplit = 64 * kDecodeBlock;
 // Parallel key generation: 64 lanes per frame, jump levels log2(64); frames
 // with more flipped positions than this take the serial kernel.
 // keygen_fast_kernel: kKeygenLanes lanes per frame (kKeygenLevels = log2 of
