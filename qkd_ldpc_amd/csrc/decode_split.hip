@@ -63,6 +63,18 @@ struct SegWeights {
     }
 };
 
+// The extrinsic interval sum of a speculative check phase: sum over k < DC of
+// row[start + k] times its weight (0 or 1, exact), in ascending order (a
+// pairwise tree, depth ~log2(DC) for two more operations, measured no faster:
+// DESIGN.md §4.3). The caller charges its rounding relative to the sum.
+template <int DC>
+__device__ __forceinline__ qkds::f2 seg_sum(const double* row, int start, const SegWeights<DC>& wk) {
+    qkds::f2 sum = qkds::f2{0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < DC; ++k) sum = __builtin_elementwise_fma(qkds::unpack_iv(row[start + k]), qkds::f2(wk[k]), sum);
+    return sum;
+}
+
 // One workgroup's message slots: x < S in LDS, the rest in global memory
 // through a buffer descriptor. Every access issues both an LDS and a buffer
 // instruction and selects: lanes whose slot is in LDS give the buffer an
@@ -365,13 +377,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         // extrinsic sum over the other lanes of the segment (a subtraction of
         // the own term would widen the interval by the own term's width)
         // (weight of entry k: bit k of the segment's mask without this lane)
-        f2 sum = f2{0.0f, 0.0f};
-        const SegWeights<DC> wk(wtab, deg, lane - start);
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            const f2 o = qkds::unpack_iv(row[start + k]);
-            sum = __builtin_elementwise_fma(o, f2(wk[k]), sum);
-        }
+        const f2 sum = seg_sum<DC>(row, start, SegWeights<DC>(wtab, deg, lane - start));
         // widened by the binary32 roundings (relative to the sum; small
         // buckets charge every segment the bucket's count) and the
         // reference's binary64 roundings (absolute, qkd_spec.h)
@@ -513,13 +519,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         wave_lds_sync();
         const int start = pw_start(wt);
         const int deg = pw_deg(wt);
-        f2 sum = f2{0.0f, 0.0f};
-        const SegWeights<DC> wk(wtab, deg, lane - start);
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            const f2 o = qkds::unpack_iv(row[start + k]);
-            sum = __builtin_elementwise_fma(o, f2(wk[k]), sum);
-        }
+        const f2 sum = seg_sum<DC>(row, start, SegWeights<DC>(wtab, deg, lane - start));
         const float nr = DC <= 8 ? (float)(DC + 2) : (float)(deg + 2);
         const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
         f2 ext = sum + f2{-mg, mg};

@@ -53,6 +53,31 @@ constexpr float kPsiSumMax = 865.0f;       // 600 / ln 2: the reference's produc
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // [lo, hi]; packed binary32 ops
 
+// The two series of phi_core, for a binary32 value or a packed pair (every
+// operation elementwise, so a pair's halves are bit for bit the scalar
+// results), in Horner's form:
+//   series_t(x) = 1 - x/2 + x^2/6 - ... + x^6/5040   (w = 1 - e^-x = x t, x < 0.35)
+//   series_h(s) = 1 + s/3 + s^2/5 + ... + s^6/13      (2 atanh(u) = 2u h, s = u^2)
+// (Estrin's scheme, depth 3 for two more operations each, measured 1.5 %
+// slower per config-2 batch: DESIGN.md §4.3.)
+template <typename V>
+__device__ __forceinline__ V poly6(V z, float c0, float c1, float c2, float c3, float c4, float c5, float c6) {
+    V p = __builtin_elementwise_fma(z, V(c6), V(c5));
+    p = __builtin_elementwise_fma(z, p, V(c4));
+    p = __builtin_elementwise_fma(z, p, V(c3));
+    p = __builtin_elementwise_fma(z, p, V(c2));
+    p = __builtin_elementwise_fma(z, p, V(c1));
+    return __builtin_elementwise_fma(z, p, V(c0));
+}
+template <typename V>
+__device__ __forceinline__ V series_t(V x) {
+    return poly6(x, 1.0f, -0.5f, 1.0f / 6.0f, -1.0f / 24.0f, 1.0f / 120.0f, -1.0f / 720.0f, 1.0f / 5040.0f);
+}
+template <typename V>
+__device__ __forceinline__ V series_h(V s) {
+    return poly6(s, 1.0f, 1.0f / 3.0f, 0.2f, 1.0f / 7.0f, 1.0f / 9.0f, 1.0f / 11.0f, 1.0f / 13.0f);
+}
+
 // phi (PSI: phi / ln 2) and an upper bound of |phi'(x)| = 1 / sinh(x)
 // (within a factor 2) at 0 < x <= kPhiHuge from u = e^-x (accurate) and x
 // (for the small-x series and the branch only).
@@ -66,12 +91,7 @@ __device__ __forceinline__ PhiVal phi_core(float x, float u) {
     // w = 1 - u: direct for x >= 0.35 (u <= 0.705: the subtraction costs under
     // a bit), below it the series x (1 - x/2 + x^2/6 - ... + x^6/5040)
     // (truncation < x^7 / 40320 < 1.7e-8 relative)
-    float t = __builtin_fmaf(x, 1.0f / 5040.0f, -1.0f / 720.0f);
-    t = __builtin_fmaf(x, t, 1.0f / 120.0f);
-    t = __builtin_fmaf(x, t, -1.0f / 24.0f);
-    t = __builtin_fmaf(x, t, 1.0f / 6.0f);
-    t = __builtin_fmaf(x, t, -0.5f);
-    t = __builtin_fmaf(x, t, 1.0f);
+    const float t = series_t(x);
     const float w = x < 0.35f ? x * t : 1.0f - u;
     const float w2 = 2.0f - w;
     const float rw = __builtin_amdgcn_rcpf(w);
@@ -84,12 +104,7 @@ __device__ __forceinline__ PhiVal phi_core(float x, float u) {
     // x >= 1: phi = 2 atanh(u) = 2u (1 + s/3 + s^2/5 + ... + s^6/13), s = u^2 <= e^-2
     // (truncation < s^7 / 15 (1 + s) < 6.4e-8 relative, under 7 % of kPhiRel)
     const float s = u * u;
-    float h = __builtin_fmaf(s, 1.0f / 13.0f, 1.0f / 11.0f);
-    h = __builtin_fmaf(s, h, 1.0f / 9.0f);
-    h = __builtin_fmaf(s, h, 1.0f / 7.0f);
-    h = __builtin_fmaf(s, h, 0.2f);
-    h = __builtin_fmaf(s, h, 1.0f / 3.0f);
-    h = __builtin_fmaf(s, h, 1.0f);
+    const float h = series_h(s);
     const float vhi = (u * (PSI ? 2.0f * kInvLn2 : 2.0f)) * h;
     PhiVal o;
     o.v = x < 1.0f ? vlo : vhi;
@@ -157,12 +172,7 @@ struct PhiVal2 {
 };
 template <bool PSI1 = false>   // half 1 in psi units too
 __device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u) {
-    f2 t = __builtin_elementwise_fma(x, f2(1.0f / 5040.0f), f2(-1.0f / 720.0f));
-    t = __builtin_elementwise_fma(x, t, f2(1.0f / 120.0f));
-    t = __builtin_elementwise_fma(x, t, f2(-1.0f / 24.0f));
-    t = __builtin_elementwise_fma(x, t, f2(1.0f / 6.0f));
-    t = __builtin_elementwise_fma(x, t, f2(-0.5f));
-    t = __builtin_elementwise_fma(x, t, f2(1.0f));
+    const f2 t = series_t(x);
     const f2 ws = x * t;
     const f2 wd = f2(1.0f) - u;
     const f2 w = f2{x.x < 0.35f ? ws.x : wd.x, x.y < 0.35f ? ws.y : wd.y};
@@ -172,12 +182,7 @@ __device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u) {
     const float lg1 = __builtin_amdgcn_logf(arg.y);
     const f2 vlo = f2{__builtin_amdgcn_logf(arg.x), PSI1 ? lg1 : kLn2 * lg1};
     const f2 s = u * u;
-    f2 h = __builtin_elementwise_fma(s, f2(1.0f / 13.0f), f2(1.0f / 11.0f));
-    h = __builtin_elementwise_fma(s, h, f2(1.0f / 9.0f));
-    h = __builtin_elementwise_fma(s, h, f2(1.0f / 7.0f));
-    h = __builtin_elementwise_fma(s, h, f2(0.2f));
-    h = __builtin_elementwise_fma(s, h, f2(1.0f / 3.0f));
-    h = __builtin_elementwise_fma(s, h, f2(1.0f));
+    const f2 h = series_h(s);
     const f2 vhi = (u * f2{2.0f * kInvLn2, PSI1 ? 2.0f * kInvLn2 : 2.0f}) * h;
     PhiVal2 o;
     o.v = f2{x.x < 1.0f ? vlo.x : vhi.x, x.y < 1.0f ? vlo.y : vhi.y};
