@@ -1407,6 +1407,7 @@ qkd_status qkd_decode_batch(const qkd_code* c, qkd_workspace* ws, const double* 
     if (!ws) return set_error(QKD_ERR_OUT_OF_MEMORY, "no workspace");
     WsSession sess(ws, (hipStream_t)stream);
     DecodeArgs a{};
+    a.pinf = std::numeric_limits<float>::infinity();
     a.n_frames = (uint32_t)n_frames;
     a.max_it = max_iterations;
     a.thr = msg_threshold;
@@ -1432,6 +1433,7 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
                               uint32_t max_it, double thr, uint32_t flags, uint8_t* bits_out,
                               uint32_t* iters, uint8_t* sp_ok, uint8_t* key_ok, hipStream_t stream) {
     DecodeArgs a{};
+    a.pinf = std::numeric_limits<float>::infinity();
     a.n_frames = (uint32_t)n_frames;
     a.max_it = max_it;
     a.thr = thr;
@@ -1942,6 +1944,7 @@ qkd_status qkd_trace_decode(const qkd_code* c, const double* llr, const uint8_t*
         return set_error(QKD_ERR_DEVICE, "trace: %s", hipGetErrorString(e));
     }
     DecodeArgs a{};
+    a.pinf = std::numeric_limits<float>::infinity();
     a.n_frames = 1;
     a.max_it = max_iterations;
     a.thr = msg_threshold;

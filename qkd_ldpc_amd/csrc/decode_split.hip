@@ -697,7 +697,11 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 f2 T = L;
                 // max(|lo|, |hi|) of an interval lo <= hi is max(hi, -lo) (med3
                 // with +inf: a max without canonicalising its operands)
-                auto amax = [](f2 x) { return __builtin_amdgcn_fmed3f(x.y, -x.x, __builtin_inff()); };
+                // (+inf from a kernel argument: with a literal one LLVM folds
+                // the med3 into a maxnum, which in IEEE mode canonicalises both
+                // operands first, three instructions for one)
+                const float pinf = a.pinf;
+                auto amax = [pinf](f2 x) { return __builtin_amdgcn_fmed3f(x.y, -x.x, pinf); };
                 float mag = amax(L);
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) {

@@ -117,6 +117,7 @@ struct DecodeArgs {
     // that fell back to the exact iterations
     uint32_t spec_cap;
     float lp_dn, lp_up, thr_dn, thr_up;
+    float pinf;          // +inf (an operand the compiler cannot fold: decode_split.hip)
     unsigned long long* spec_replays;
     // frames replayed exactly in this launch (zeroed per launch): once they
     // pass a quarter of the frames started, later frames skip the speculation
