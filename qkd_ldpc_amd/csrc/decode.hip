@@ -1169,6 +1169,49 @@ static hipError_t decoder_event(qkd_workspace* ws, hipStream_t stream) {
     return hipEventRecord(ws->dec_ev[ws->dec_ev_used++], stream);
 }
 
+// DeviceCode::plan_slot with its slot words encoded for a split-kernel layout
+// (encode_slot, binary64 slots), built on a layout's first launch and kept
+// with the code
+static qkd_status plan_for_layout(const qkd_code* c, const SplitLds& L, const uint2** out) {
+    std::lock_guard<std::mutex> lock(c->plan_mu);
+    const auto key = std::make_pair(L.S, (uint32_t)L.msg);
+    auto it = c->d_plan_enc.find(key);
+    if (it == c->d_plan_enc.end()) {
+        std::vector<uint2> enc(c->plan_slot_host);
+        for (uint2& w : enc) w.x = encode_slot(w.x, L.S, (uint32_t)L.msg, (uint32_t)sizeof(double));
+        uint2* d = nullptr;
+        if (hipMalloc(&d, enc.size() * sizeof(uint2)) != hipSuccess)
+            return set_error(QKD_ERR_OUT_OF_MEMORY, "code: cannot allocate %zu B for an encoded plan",
+                             enc.size() * sizeof(uint2));
+        if (hipMemcpy(d, enc.data(), enc.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return set_error(QKD_ERR_DEVICE, "code: encoded plan upload failed");
+        }
+        it = c->d_plan_enc.emplace(key, d).first;
+    }
+    *out = it->second;
+    return QKD_OK;
+}
+
+// The split kernels' encoded slot words are absolute LDS addresses: their
+// dynamic LDS must start at address 0, i.e. no static LDS (checked once per
+// kernel).
+static qkd_status check_no_static_lds(DecodeFn fn) {
+    static std::mutex mu;
+    static std::map<const void*, size_t> seen;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = seen.find((const void*)fn);
+    if (it == seen.end()) {
+        hipFuncAttributes fa{};
+        QKD_HIP(hipFuncGetAttributes(&fa, (const void*)fn));
+        it = seen.emplace((const void*)fn, fa.sharedSizeBytes).first;
+    }
+    if (it->second != 0)
+        return set_error(QKD_ERR_UNSUPPORTED, "split decoder with %zu B of static LDS (its slot words "
+                                              "address LDS from 0)", it->second);
+    return QKD_OK;
+}
+
 static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs& a, int mode,
                                 uint32_t flags, hipStream_t stream) {
     int dc = 0;
@@ -1227,6 +1270,11 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             if (s != QKD_OK) return s;
             a.code = c->view();
             a.c2b = ws->c2b;
+            a.plan_enc = nullptr;
+            if (rule == kRuleSp64) {
+                s = plan_for_layout(c, L, &a.plan_enc);
+                if (s != QKD_OK) return s;
+            }
             const size_t slots = (size_t)c->max_dv * c->n_pad;
             // elements of the message type, plus kC2bPad: the workgroups' regions
             // start off a common alignment (measured: config 2 with the fold table
@@ -1276,6 +1324,10 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                     a.ckpt = ws->ckpt;
                     a.ckpt_stride = (uint32_t)slots;
                 }
+            }
+            if (rule == kRuleSp64) {
+                s = check_no_static_lds(sfn);
+                if (s != QKD_OK) return s;
             }
             QKD_HIP(decoder_event(ws, stream));
             hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);

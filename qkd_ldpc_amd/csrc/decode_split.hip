@@ -75,6 +75,28 @@ __device__ __forceinline__ qkds::f2 seg_sum(const double* row, int start, const 
     return sum;
 }
 
+// Lane `lane`'s word of plan task t through a buffer descriptor: the task's
+// offset is a scalar operand and the lane's a loop-invariant VGPR, so a load
+// costs no vector address arithmetic (a pointer form becomes a 64-bit VGPR
+// induction variable, two adds per load). t is wave-uniform; readfirstlane
+// says so where the compiler cannot prove it (else it emits a waterfall loop).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plan_rsrc(const uint2* plan) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(plan), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ uint2 plan_word(__amdgpu_buffer_rsrc_t plan, int t, int lane) {
+    using V = decltype(__builtin_amdgcn_raw_buffer_load_b64(plan, 0, 0, 0));
+    const V v = __builtin_amdgcn_raw_buffer_load_b64(plan, (int)((uint32_t)lane * 8u),
+                                                       __builtin_amdgcn_readfirstlane(t * 64 * 8), 0);
+    return __builtin_bit_cast(uint2, v);
+}
+
+// [lo, hi] negated: [-hi, -lo] when neg. Written per element, so each half is
+// one v_cndmask_b32 with a negated source (the vector form costs a packed
+// negation and a swap besides).
+__device__ __forceinline__ qkds::f2 neg_iv_if(bool neg, qkds::f2 v) {
+    return qkds::f2{neg ? -v.y : v.x, neg ? -v.x : v.y};
+}
+
 // One workgroup's message slots: x < S in LDS, the rest in global memory
 // through a buffer descriptor. Every access issues both an LDS and a buffer
 // instruction and selects: lanes whose slot is in LDS give the buffer an
@@ -119,6 +141,40 @@ struct SplitStore {
         const T vg = BufIo<T>::ld(g, (x - S) * (uint32_t)sizeof(T));
         return in ? vl : vg;
     }
+    // The check phases address slots by encoded words (encode_slot,
+    // qkd_decode.h; DecodeArgs::plan_enc): an LDS slot's word is its byte
+    // address with kSlotLds set, which the buffer range check rejects; a
+    // global slot's word is its byte offset in the region past
+    // kSlotGlobalBase, an LDS address past any allocation (the hardware
+    // returns 0 and drops the store there, tools/mb/lds_oob.hip). So both
+    // accesses take the word as it is (the LDS one without its top bit), and
+    // a load is the OR of the two halves: no compare, no select.
+    __amdgpu_buffer_rsrc_t gw;   // the region, kSlotGlobalBase bytes before its start
+    // ld_w in two halves for a software pipeline: ld_raw issues both accesses,
+    // pick (at the value's first use, a loop iteration later) combines them
+    struct Raw {
+        T vl, vg;
+    };
+    // (the byte addresses are absolute: the dynamic LDS starts at address 0,
+    // the split kernels having no static LDS, which the host checks)
+    typedef __attribute__((address_space(3))) T LdsT;
+    __device__ __forceinline__ LdsT* lds_of(uint32_t w) const {
+        return reinterpret_cast<LdsT*>((size_t)(w & ~kSlotLds));
+    }
+    __device__ __forceinline__ Raw ld_raw(uint32_t w) const {
+        return Raw{*lds_of(w), BufIo<T>::ld(gw, w)};
+    }
+    __device__ __forceinline__ T pick(const Raw& r) const {
+        if constexpr (sizeof(T) == 8)
+            return __builtin_bit_cast(T, __builtin_bit_cast(uint64_t, r.vl) | __builtin_bit_cast(uint64_t, r.vg));
+        else
+            return __builtin_bit_cast(T, __builtin_bit_cast(uint32_t, r.vl) | __builtin_bit_cast(uint32_t, r.vg));
+    }
+    __device__ __forceinline__ T ld_w(uint32_t w) const { return pick(ld_raw(w)); }
+    __device__ __forceinline__ void st_w(uint32_t w, T v) const {
+        *lds_of(w) = v;
+        BufIo<T>::st(gw, w, v);
+    }
     __device__ __forceinline__ void st(uint32_t x, T v) const {
         if constexpr (ALL) {
             l[x] = v;
@@ -157,7 +213,7 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
     constexpr int NW = kDecodeBlock / 64;
     int t = wave;
     if (t >= n_tasks) return;
-    const uint2* pl = plan + lane;
+    const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
     auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
     auto sbit = [&](uint2 p) -> uint32_t {
         const uint32_t j = pw_chk(p);
@@ -173,30 +229,30 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
         wave_lds_sync();
         return edge_out<CLAMP, DC, RULE>(a, w, sbit(w), lane, thr, row, 0.0f);
     };
-    uint2 wa = pl[t * 64];
-    uint2 wb = pl[(t + NW) * 64];
-    T xa = ms.ld(slot(wa));
+    uint2 wa = plan_word(prs, t, lane);
+    uint2 wb = plan_word(prs, t + NW, lane);
+    auto xa = ms.ld_raw(slot(wa));
     uint32_t pend = 0xffffffffu;    // slot of the previous task's message, not yet stored
     T pv = 0;
     for (;;) {
-        if (pend != 0xffffffffu) ms.st(pend, pv);
-        const uint2 wc = pl[(t + 2 * NW) * 64];
-        const T xb = ms.ld(slot(wb));
-        pv = edge(xa, wa);
+        if (pend != 0xffffffffu) ms.st_w(pend, pv);
+        const uint2 wc = plan_word(prs, t + 2 * NW, lane);
+        const auto xb = ms.ld_raw(slot(wb));
+        pv = edge(ms.pick(xa), wa);
         pend = slot(wa);
         t += NW;
         if (t >= n_tasks) break;
-        ms.st(pend, pv);
-        wa = pl[(t + 2 * NW) * 64];
-        xa = ms.ld(slot(wc));
-        pv = edge(xb, wb);
+        ms.st_w(pend, pv);
+        wa = plan_word(prs, t + 2 * NW, lane);
+        xa = ms.ld_raw(slot(wc));
+        pv = edge(ms.pick(xb), wb);
         pend = slot(wb);
         t += NW;
         if (t >= n_tasks) break;
         wb = wa;
         wa = wc;
     }
-    ms.st(pend, pv);
+    ms.st_w(pend, pv);
 }
 
 // ---- the binary32 variant (kRuleSp32; specification: tests/test_variants.py) 
@@ -215,19 +271,19 @@ __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan,
     constexpr int NW = kDecodeBlock / 64;
     int t = wave;
     if (t >= n_tasks) return;
-    const uint2* pl = plan + lane;
+    const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
     if (lane < DC) row[64 + lane] = 0.0f;
     auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
-    uint2 wt = pl[t * 64];
-    uint2 wn = pl[(t + NW) * 64];
-    uint2 wnn = pl[(t + 2 * NW) * 64];
+    uint2 wt = plan_word(prs, t, lane);
+    uint2 wn = plan_word(prs, t + NW, lane);
+    uint2 wnn = plan_word(prs, t + 2 * NW, lane);
     float xt = ms.ld(slot(wt));
     row[lane] = __builtin_fabsf(RuleMath<kRuleSp32>::tanh_half(xt));
     uint64_t sgn_t = __ballot(xt < 0.0f);
     bool neg_t = xt < 0.0f;
     float xn = ms.ld(slot(wn));
     for (;;) {
-        const uint2 w3 = pl[(t + 3 * NW) * 64];
+        const uint2 w3 = plan_word(prs, t + 3 * NW, lane);
         const float xnn = ms.ld(slot(wnn));
         wave_lds_sync();
         const int start = pw_start(wt);
@@ -348,14 +404,14 @@ template <int DC>
 __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ plan, const uint32_t* tsyn,
                                                  const SplitStore<double>& ms, double* row, const float* wtab,
                                                  int n_tasks,
-                                                 uint32_t n_pad, uint32_t n_bits, float thr_dn, float thr_up,
+                                                 uint32_t n_pad, uint32_t dummy, float thr_dn, float thr_up,
                                                  uint32_t* round_word, int wave, int lane) {
     using qkds::f2;
     constexpr int NW = kDecodeBlock / 64;
     int t = wave;
     if (t >= n_tasks) return;
+    const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
     bool bad = false;
-    const uint2* pl = plan + lane;
     // the row's DC entries past lane 63 are read (times 0) by segments ending
     // there: keep them finite (the prologue stages key words in this region)
     if (lane < DC) row[64 + lane] = 0.0;
@@ -367,8 +423,8 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         const f2 bv = qkds::unpack_iv(xv);
         const bool neg = bv.x < 0.0f;
         const bool ok = bv.x == bv.x;
-        bad |= !ok && pw_slot(w) != n_bits;
-        const f2 ph = ok ? (neg ? -bv.yx : bv) : f2{0.0f, 0.0f};
+        bad |= !ok && pw_slot(w) != dummy;
+        const f2 ph = ok ? neg_iv_if(neg, bv) : f2{0.0f, 0.0f};
         row[lane] = qkds::pack_iv(ph);
         const uint64_t sgn = __ballot(neg);
         wave_lds_sync();
@@ -396,59 +452,32 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
         const uint32_t sigma =
             sj ^ (uint32_t)(DC < 32 ? seg_parity32(sgn, w) : seg_parity(sgn, w)) ^ (neg ? 1u : 0u);
-        return qkds::pack_iv(sigma ? -m.yx : m);
+        return qkds::pack_iv(neg_iv_if(sigma != 0u, m));
     };
-#ifndef QKD_PSI_LA
-#define QKD_PSI_LA 1
-#endif
-    if constexpr (QKD_PSI_LA >= 2) {
-        // slots two tasks ahead, plan words three (the global slots' L2
-        // latency under the kernel's own store traffic)
-        uint2 w0 = pl[t * 64], w1 = pl[(t + NW) * 64], w2 = pl[(t + 2 * NW) * 64];
-        double x0 = ms.ld(slot(w0)), x1 = ms.ld(slot(w1));
-        uint32_t pend = 0xffffffffu;
-        double pv = 0;
-        for (;;) {
-            const uint2 w3 = pl[(t + 3 * NW) * 64];
-            const double x2 = ms.ld(slot(w2));
-            if (pend != 0xffffffffu) ms.st(pend, pv);
-            pv = edge(x0, w0);
-            pend = slot(w0);
-            t += NW;
-            if (t >= n_tasks) break;
-            w0 = w1;
-            w1 = w2;
-            w2 = w3;
-            x0 = x1;
-            x1 = x2;
-        }
-        ms.st(pend, pv);
-    } else {
-    uint2 wa = pl[t * 64];
-    uint2 wb = pl[(t + NW) * 64];
-    double xa = ms.ld(slot(wa));
+    uint2 wa = plan_word(prs, t, lane);
+    uint2 wb = plan_word(prs, t + NW, lane);
+    auto xa = ms.ld_raw(slot(wa));
     uint32_t pend = 0xffffffffu;
     double pv = 0;
     for (;;) {
-        if (pend != 0xffffffffu) ms.st(pend, pv);
-        const uint2 wc = pl[(t + 2 * NW) * 64];
-        const double xb = ms.ld(slot(wb));
-        pv = edge(xa, wa);
+        if (pend != 0xffffffffu) ms.st_w(pend, pv);
+        const uint2 wc = plan_word(prs, t + 2 * NW, lane);
+        const auto xb = ms.ld_raw(slot(wb));
+        pv = edge(ms.pick(xa), wa);
         pend = slot(wa);
         t += NW;
         if (t >= n_tasks) break;
-        ms.st(pend, pv);
-        wa = pl[(t + 2 * NW) * 64];
-        xa = ms.ld(slot(wc));
-        pv = edge(xb, wb);
+        ms.st_w(pend, pv);
+        wa = plan_word(prs, t + 2 * NW, lane);
+        xa = ms.ld_raw(slot(wc));
+        pv = edge(ms.pick(xb), wb);
         pend = slot(wb);
         t += NW;
         if (t >= n_tasks) break;
         wb = wa;
         wa = wc;
     }
-    ms.st(pend, pv);
-    }
+    ms.st_w(pend, pv);
     if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
 }
 
@@ -464,14 +493,14 @@ template <int DC>
 __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict__ plan, const uint32_t* tsyn,
                                                         const SplitStore<double>& ms, double* row, const float* wtab,
                                                         int n_tasks,
-                                                        uint32_t n_pad, uint32_t n_bits, float thr_dn, float thr_up,
+                                                        uint32_t n_pad, uint32_t dummy, float thr_dn, float thr_up,
                                                         uint32_t* round_word, int wave, int lane) {
     using qkds::f2;
     constexpr int NW = kDecodeBlock / 64;
     int t = wave;
     if (t >= n_tasks) return;
+    const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
     bool bad = false;
-    const uint2* pl = plan + lane;
     if (lane < DC) row[64 + lane] = 0.0;
     auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
     // |b2c| of an edge, its sign and whether the interval certifies it
@@ -479,46 +508,40 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
     auto input = [&](double xv, uint2 w, bool& neg, f2& ab) -> bool {
         const f2 bv = qkds::unpack_iv(xv);
         neg = bv.y < 0.0f;
-        ab = neg ? -bv.yx : bv;
+        ab = neg_iv_if(neg, bv);
         const bool ok = (neg || bv.x > 0.0f) && ab.x > 1.0e-30f;
-        bad |= !ok && pw_slot(w) != n_bits;
+        bad |= !ok && pw_slot(w) != dummy;
         return ok;
     };
     // (the plan has kPlanPadTasks idle tasks past n_tasks: loads ahead need no test)
-    uint2 wt = pl[t * 64];
-    uint2 wn = pl[(t + NW) * 64];
-    uint2 wnn = pl[(t + 2 * NW) * 64];
+    uint2 wt = plan_word(prs, t, lane);
+    uint2 wn = plan_word(prs, t + NW, lane);
+    uint2 wnn = plan_word(prs, t + 2 * NW, lane);
     bool neg_t;
     {
         f2 ab;
-        const bool ok = input(ms.ld(slot(wt)), wt, neg_t, ab);
+        const bool ok = input(ms.ld_w(slot(wt)), wt, neg_t, ab);
         row[lane] = qkds::pack_iv(ok ? qkds::phi_bounds(ab.x, ab.y) : f2{0.0f, 0.0f});
     }
     uint64_t sgn_t = __ballot(neg_t);
-    double xn = ms.ld(slot(wn));
-#ifndef QKD_PAIR_LA
-#define QKD_PAIR_LA 2
-#endif
-    // (QKD_PAIR_LA 3: slots three tasks ahead, plan words four)
-    uint2 w3 = pl[(t + 3 * NW) * 64];
-    double xnn = QKD_PAIR_LA >= 3 ? ms.ld(slot(wnn)) : 0.0;
-    for (;;) {
-        uint2 w4;
-        double x3;
-        if constexpr (QKD_PAIR_LA >= 3) {
-            w4 = pl[(t + 4 * NW) * 64];
-            x3 = ms.ld(slot(w3));
-        } else {
-            w3 = pl[(t + 3 * NW) * 64];
-            xnn = ms.ld(slot(wnn));
-        }
+    using Raw = SplitStore<double>::Raw;
+    // One task: task t's c2b from the row and the input bound of task t + NW
+    // (its slot x_n, loaded one task earlier) into the row; loads the plan
+    // word three tasks ahead (into w_ld) and the slot of task t + 2 NW (into
+    // x_ld). The loop runs it unrolled four times over four plan-word and two
+    // slot registers, so nothing is copied between tasks and each slot's
+    // select waits one task after its load (SplitStore::pick).
+    auto step = [&](const uint2 w_t, const uint2 w_n, const uint2 w_nn, uint2& w_ld, const Raw& x_n,
+                    Raw& x_ld) -> bool {
+        w_ld = plan_word(prs, t + 3 * NW, lane);
+        x_ld = ms.ld_raw(slot(w_nn));
         bool neg_n;
         f2 ab_n;
-        const bool ok_n = input(xn, wn, neg_n, ab_n);
+        const bool ok_n = input(ms.pick(x_n), w_n, neg_n, ab_n);
         // this task's extrinsic sums (as spec_check_phase_psi)
         wave_lds_sync();
-        const int start = pw_start(wt);
-        const int deg = pw_deg(wt);
+        const int start = pw_start(w_t);
+        const int deg = pw_deg(w_t);
         const f2 sum = seg_sum<DC>(row, start, SegWeights<DC>(wtab, deg, lane - start));
         const float nr = DC <= 8 ? (float)(DC + 2) : (float)(deg + 2);
         const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
@@ -530,25 +553,25 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         // this task's c2b: threshold_matrix (:246-249) on the magnitude, the sign
         m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
         m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
-        const uint32_t j = pw_chk(wt);
+        const uint32_t j = pw_chk(w_t);
         const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
         const uint32_t sigma =
-            sj ^ (uint32_t)(DC < 32 ? seg_parity32(sgn_t, wt) : seg_parity(sgn_t, wt)) ^ (neg_t ? 1u : 0u);
-        ms.st(slot(wt), qkds::pack_iv(sigma ? -m.yx : m));
+            sj ^ (uint32_t)(DC < 32 ? seg_parity32(sgn_t, w_t) : seg_parity(sgn_t, w_t)) ^ (neg_t ? 1u : 0u);
+        ms.st_w(slot(w_t), qkds::pack_iv(neg_iv_if(sigma != 0u, m)));
         // the next task's input bounds into the row
         row[lane] = qkds::pack_iv(ok_n ? ph_n : f2{0.0f, 0.0f});
         sgn_t = __ballot(neg_n);
         neg_t = neg_n;
         t += NW;
-        if (t >= n_tasks) break;
-        wt = wn;
-        wn = wnn;
-        wnn = w3;
-        xn = xnn;
-        if constexpr (QKD_PAIR_LA >= 3) {
-            w3 = w4;
-            xnn = x3;
-        }
+        return t < n_tasks;
+    };
+    Raw xa = ms.ld_raw(slot(wn)), xb;
+    uint2 wd;
+    for (;;) {
+        if (!step(wt, wn, wnn, wd, xa, xb)) break;
+        if (!step(wn, wnn, wd, wt, xb, xa)) break;
+        if (!step(wnn, wd, wt, wn, xa, xb)) break;
+        if (!step(wd, wt, wn, wnn, xb, xa)) break;
     }
     if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
 }
@@ -838,11 +861,18 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
         wtab[e] = (k < deg && k != p) ? 1.0f : 0.0f;
     }
     using MS = SplitStore<T, RULE == kRuleSp32>;
+    T* const region = reinterpret_cast<T*>(a.c2b) + (size_t)region_of_block() * a.c2b_stride;
     const MS ms{
         reinterpret_cast<T*>(smem + L.msg),
-        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<T*>(a.c2b) + (size_t)region_of_block() * a.c2b_stride, (short)0,
-                                          (int)(a.c2b_stride * sizeof(T)), 0x00020000),
-        L.S};
+        __builtin_amdgcn_make_buffer_rsrc(region, (short)0, (int)(a.c2b_stride * sizeof(T)), 0x00020000),
+        L.S,
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(region) - kSlotGlobalBase, (short)0,
+                                          (int)(kSlotGlobalBase + a.c2b_stride * sizeof(T)), 0x00020000)};
+    // the check phases' plan: encoded slot words for this layout (binary64
+    // rule: DecodeArgs::plan_enc, built by the host from L), slot indices for
+    // the all-LDS binary32 rule; the dummy column's slot in the same form
+    const uint2* const plan = RULE == kRuleSp64 ? a.plan_enc : c.plan_slot;
+    const uint32_t dummy_w = encode_slot((uint32_t)c.n, L.S, (uint32_t)L.msg, (uint32_t)sizeof(T));
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1013,11 +1043,11 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     // (iteration 2 after the folded first one: the slots hold
                     // the phi bounds of exact b2c, psi_of_exact)
                     if (!folded && fold1 && it == 1) {
-                        spec_check_phase_psi<DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n,
+                        spec_check_phase_psi<DC>(plan, tsyn, ms, row, wtab, n_tasks, n_pad, dummy_w,
                                                  a.thr_dn, a.thr_up, rw, wave, lane);
                         __syncthreads();
                     } else if (!folded) {
-                        spec_check_phase_paired<DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, (uint32_t)c.n, a.thr_dn,
+                        spec_check_phase_paired<DC>(plan, tsyn, ms, row, wtab, n_tasks, n_pad, dummy_w, a.thr_dn,
                                                     a.thr_up, rw, wave, lane);
                         __syncthreads();
                     }
@@ -1026,10 +1056,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                 if constexpr (RULE == kRuleSp32)
                     sp32_check_phase<CLAMP, DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, thr, wave, lane);
                 else if (TABLES && it == 1 && tab2_on)
-                    split_check_phase<kSrcTable, CLAMP, DC, RULE>(c.plan_slot, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
+                    split_check_phase<kSrcTable, CLAMP, DC, RULE>(plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);
                 else
-                    split_check_phase<kSrcFirst, CLAMP, DC, RULE>(c.plan_slot, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
+                    split_check_phase<kSrcFirst, CLAMP, DC, RULE>(plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
                                                                    wave, lane);
                 __syncthreads();
             }

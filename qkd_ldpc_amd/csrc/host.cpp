@@ -52,6 +52,8 @@ static void free_device(qkd_code* c) {
     c->d_plan = nullptr;
     if (c->d_plan_slot) (void)hipFree(c->d_plan_slot);
     c->d_plan_slot = nullptr;
+    for (auto& kv : c->d_plan_enc) (void)hipFree(kv.second);
+    c->d_plan_enc.clear();
     if (c->d_jump) (void)hipFree(c->d_jump);
     c->d_jump = nullptr;
     if (c->d_jpoly) (void)hipFree(c->d_jpoly);
@@ -226,6 +228,7 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         plan2[k].x = (plan.word[k] >> 24) * (uint32_t)c->n_pad + (plan.word[k] & qkdp::kPlanBitMask);
     QKD_HIP(hipMalloc(&c->d_plan_slot, plan2.size() * sizeof(uint2)));
     QKD_HIP(hipMemcpy(c->d_plan_slot, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    c->plan_slot_host = std::move(plan2);
     // Key-generation jump-ahead: chunk = draws per lane, a multiple of 64 so
     // every lane's Alice bits fill whole words.
     const uint64_t draws = qkdr::trial_draws((uint32_t)n);

@@ -105,6 +105,9 @@ struct DecodeArgs {
     size_t totals_stride;
     // decode_split_kernel: the LDS budget its layout was sized for (SplitLds)
     uint32_t lds_budget;
+    // decode_split_kernel, binary64 rule: DeviceCode::plan_slot with the slot
+    // field encoded for this launch's layout (encode_slot)
+    const uint2* plan_enc;
     // decode_split_kernel, kModeKeys: per frame 2 * m_words syndrome words
     // from frame_syn_kernel (target s_A, then the first-product signs), and
     // the frame's last hard decision out as packed words (key_match_kernel
@@ -521,6 +524,20 @@ struct SplitLds {
         bytes = msg + ((size_t)S + 64) * esz;
     }
 };
+
+// Encoded message-slot words of the split decoder's check phases (its plan,
+// DecodeArgs::plan_enc, one per LDS layout): slot x < S (in LDS) as
+// kSlotLds | its byte address from the dynamic LDS base; a global slot as
+// kSlotGlobalBase + its byte offset in the workgroup's region. The buffer
+// descriptor of the region starts kSlotGlobalBase bytes early and spans
+// kSlotGlobalBase + the region, so LDS words fail its range check (loads give
+// 0, stores are dropped), and global words are LDS addresses past any
+// allocation (the same there: tools/mb/lds_oob.hip measures it on gfx950).
+constexpr uint32_t kSlotLds = 0x80000000u;
+constexpr uint32_t kSlotGlobalBase = 0x40000u;
+__host__ __device__ inline uint32_t encode_slot(uint32_t x, uint32_t S, uint32_t msg, uint32_t esz) {
+    return x < S ? (kSlotLds | (msg + x * esz)) : (kSlotGlobalBase + (x - S) * esz);
+}
 
 using DecodeFn = void (*)(DecodeArgs);
 // decode_split.hip: the split-store kernel for (mode, rule in {kRuleSp64,

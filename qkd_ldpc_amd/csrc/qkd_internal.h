@@ -148,6 +148,12 @@ struct qkd_code {
     uint8_t* d_bit_deg = nullptr;
     uint2* d_plan = nullptr;
     uint2* d_plan_slot = nullptr;
+    // the slot plan on the host, and its encoded forms by LDS layout
+    // ((S, message base) -> device copy, qkd::plan_for_layout; plan_mu guards
+    // the map: workspaces on several threads may share the code)
+    std::vector<uint2> plan_slot_host;
+    mutable std::map<std::pair<uint32_t, uint32_t>, uint2*> d_plan_enc;
+    mutable std::mutex plan_mu;
     int32_t n_pat = 0;                  // 0: too many degree patterns for the table
     std::vector<uint8_t> pat_deg;
     uint16_t* d_bit_pat = nullptr;
