@@ -1169,16 +1169,21 @@ static hipError_t decoder_event(qkd_workspace* ws, hipStream_t stream) {
     return hipEventRecord(ws->dec_ev[ws->dec_ev_used++], stream);
 }
 
-// DeviceCode::plan_slot with its slot words encoded for a split-kernel layout
-// (encode_slot, binary64 slots), built on a layout's first launch and kept
-// with the code
-static qkd_status plan_for_layout(const qkd_code* c, const SplitLds& L, const uint2** out) {
+// DeviceCode::plan_slot encoded for a split-kernel layout and check-degree
+// bucket: slot words by encode_slot (binary64 slots), segment words by
+// encode_seg; built on a layout's first launch and kept with the code
+static qkd_status plan_for_layout(const qkd_code* c, const SplitLds& L, int dc, const uint2** out) {
     std::lock_guard<std::mutex> lock(c->plan_mu);
-    const auto key = std::make_pair(L.S, (uint32_t)L.msg);
+    const auto key = std::make_pair(L.S, ((uint32_t)L.msg << 8) | (uint32_t)dc);
     auto it = c->d_plan_enc.find(key);
     if (it == c->d_plan_enc.end()) {
         std::vector<uint2> enc(c->plan_slot_host);
-        for (uint2& w : enc) w.x = encode_slot(w.x, L.S, (uint32_t)L.msg, (uint32_t)sizeof(double));
+        for (size_t k = 0; k < enc.size(); ++k) {
+            uint2& w = enc[k];
+            w.x = encode_slot(w.x, L.S, (uint32_t)L.msg, (uint32_t)sizeof(double));
+            w.y = encode_seg(w.y & qkdp::kPlanChkMask, (w.y >> 20) & 63u, (w.y >> 26) + 1, (uint32_t)(k & 63),
+                             (uint32_t)dc);
+        }
         uint2* d = nullptr;
         if (hipMalloc(&d, enc.size() * sizeof(uint2)) != hipSuccess)
             return set_error(QKD_ERR_OUT_OF_MEMORY, "code: cannot allocate %zu B for an encoded plan",
@@ -1233,7 +1238,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     // kernel's store.
     const char* kern = getenv("QKD_DECODE_KERNEL");
     const bool classic = kern && !strcmp(kern, "classic");
-    if ((rule == kRuleSp64 || rule == kRuleSp32) && !classic && !a.trace && c->n <= kMaxBitsSplit) {
+    if ((rule == kRuleSp64 || rule == kRuleSp32) && !classic && !a.trace && c->n <= kMaxBitsSplit &&
+        c->m <= kMaxChecksSplit) {
         int sdc = 0;
         DecodeFn sfn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &sdc);
         const int esz = rule == kRuleSp64 ? 8 : 4;
@@ -1272,7 +1278,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             a.c2b = ws->c2b;
             a.plan_enc = nullptr;
             if (rule == kRuleSp64) {
-                s = plan_for_layout(c, L, &a.plan_enc);
+                s = plan_for_layout(c, L, sdc, &a.plan_enc);
                 if (s != QKD_OK) return s;
             }
             const size_t slots = (size_t)c->max_dv * c->n_pad;
@@ -1305,6 +1311,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             if (spec) {
                 int xdc = 0, sgrid = 0;
                 DecodeFn xfn = pick_split_spec(mode, c->max_dc, ckpt, &xdc);
+                if (xdc != sdc)      // (the layout and the encoded plan are the bucket's)
+                    return set_error(QKD_ERR_UNSUPPORTED, "speculative kernel bucket %d != %d", xdc, sdc);
                 s = decode_grid(c, xfn, L.bytes, &sgrid);
                 if (s != QKD_OK) return s;
                 sfn = xfn;

@@ -63,6 +63,40 @@ struct SegWeights {
     }
 };
 
+// A lane's segment and target bit from an encoded plan word (encode_seg).
+__device__ __forceinline__ int seg_start(uint2 w) { return (int)((w.y >> kSegStartShift) & 63u); }
+__device__ __forceinline__ uint32_t seg_wi(uint2 w) { return (w.y >> kSegWiShift) & 255u; }
+template <int DC>
+__device__ __forceinline__ int seg_deg(uint2 w) {
+    return DC <= 16 ? (int)(seg_wi(w) / (uint32_t)DC) + 1 : (int)seg_wi(w) + 1;
+}
+template <int DC>
+__device__ __forceinline__ SegWeights<DC> seg_weights(const float* wtab, uint2 w, int lane) {
+    if constexpr (DC <= 8) {
+        SegWeights<DC> r(wtab, 1, 0);
+        r.w = wtab + seg_wi(w) * DC;
+        return r;
+    } else {
+        return SegWeights<DC>(wtab, seg_deg<DC>(w), lane - seg_start(w));
+    }
+}
+// the check's target bit: its syndrome word read from LDS address 0 on (tsyn
+// leads the layout, SplitLds, and the dynamic LDS starts at 0)
+__device__ __forceinline__ uint32_t seg_sbit(uint2 w) {
+    typedef __attribute__((address_space(3))) const uint32_t LdsU32;
+    const uint32_t word = *reinterpret_cast<LdsU32*>((size_t)(w.y >> kSegWordShift));
+    return (word >> (w.y & 31u)) & 1u;
+}
+// parity of the segment's bits in a wave ballot (seg_parity of qkd_decode.h)
+template <int DC>
+__device__ __forceinline__ uint32_t seg_parity_enc(uint64_t ballot, uint2 w) {
+    const uint64_t sh = ballot >> seg_start(w);
+    const uint32_t deg = (uint32_t)seg_deg<DC>(w);
+    if constexpr (DC < 32) return (uint32_t)__popc(__builtin_amdgcn_ubfe((uint32_t)sh, 0, deg)) & 1u;
+    const uint64_t m = deg >= 64 ? ~0ull : ((1ull << deg) - 1ull);
+    return (uint32_t)__popcll(sh & m) & 1u;
+}
+
 // The extrinsic interval sum of a speculative check phase: sum over k < DC of
 // row[start + k] times its weight (0 or 1, exact), in ascending order (a
 // pairwise tree, depth ~log2(DC) for two more operations, measured no faster:
@@ -215,10 +249,6 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
     if (t >= n_tasks) return;
     const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
     auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
-    auto sbit = [&](uint2 p) -> uint32_t {
-        const uint32_t j = pw_chk(p);
-        return (tsyn[j >> 5] >> (j & 31)) & 1u;
-    };
     auto edge = [&](T x, uint2 w) -> T {
         T a;
         if constexpr (SRC == kSrcTable && RULE == kRuleSp64)
@@ -227,7 +257,9 @@ __device__ __forceinline__ void split_check_phase(const uint2* __restrict__ plan
             a = RuleMath<RULE>::tanh_half(x);                      // (:224)
         row[lane] = a;
         wave_lds_sync();
-        return edge_out<CLAMP, DC, RULE>(a, w, sbit(w), lane, thr, row, 0.0f);
+        // (edge_out reads the segment from a plan word of the unencoded form)
+        const uint2 wo = make_uint2(w.x, ((uint32_t)seg_start(w) << 20) | ((uint32_t)(seg_deg<DC>(w) - 1) << 26));
+        return edge_out<CLAMP, DC, RULE>(a, wo, seg_sbit(w), lane, thr, row, 0.0f);
     };
     uint2 wa = plan_word(prs, t, lane);
     uint2 wb = plan_word(prs, t + NW, lane);
@@ -411,7 +443,8 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
     int t = wave;
     if (t >= n_tasks) return;
     const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
-    bool bad = false;
+    // lanes that could not certify (wave masks: scalar ors, no per-lane flag)
+    uint64_t bad = 0;
     // the row's DC entries past lane 63 are read (times 0) by segments ending
     // there: keep them finite (the prologue stages key words in this region)
     if (lane < DC) row[64 + lane] = 0.0;
@@ -423,17 +456,17 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         const f2 bv = qkds::unpack_iv(xv);
         const bool neg = bv.x < 0.0f;
         const bool ok = bv.x == bv.x;
-        bad |= !ok && pw_slot(w) != dummy;
+        bad |= __ballot(!ok && pw_slot(w) != dummy);
         const f2 ph = ok ? neg_iv_if(neg, bv) : f2{0.0f, 0.0f};
         row[lane] = qkds::pack_iv(ph);
         const uint64_t sgn = __ballot(neg);
         wave_lds_sync();
-        const int start = pw_start(w);
-        const int deg = pw_deg(w);
+        const int start = seg_start(w);
+        const int deg = seg_deg<DC>(w);
         // extrinsic sum over the other lanes of the segment (a subtraction of
         // the own term would widen the interval by the own term's width)
         // (weight of entry k: bit k of the segment's mask without this lane)
-        const f2 sum = seg_sum<DC>(row, start, SegWeights<DC>(wtab, deg, lane - start));
+        const f2 sum = seg_sum<DC>(row, start, seg_weights<DC>(wtab, w, lane));
         // widened by the binary32 roundings (relative to the sum; small
         // buckets charge every segment the bucket's count) and the
         // reference's binary64 roundings (absolute, qkd_spec.h)
@@ -441,17 +474,14 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
         f2 ext = sum + f2{-mg, mg};
         ext.x = ext.x > 0.0f ? ext.x : 0.0f;
-        bad |= !(ext.y < qkds::kPsiSumMax);                // the reference's product would underflow
+        bad |= __ballot(!(ext.y < qkds::kPsiSumMax));      // the reference's product would underflow
         f2 m = qkds::phi_bounds_out(ext.x, ext.y);
         // threshold_matrix (:246-249) on the magnitude
         // (m >= 0, not NaN: med3 with 0 is the min, without the per-edge
         // canonicalisation fminf needs for a kernel argument)
         m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
         m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
-        const uint32_t j = pw_chk(w);
-        const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
-        const uint32_t sigma =
-            sj ^ (uint32_t)(DC < 32 ? seg_parity32(sgn, w) : seg_parity(sgn, w)) ^ (neg ? 1u : 0u);
+        const uint32_t sigma = seg_sbit(w) ^ seg_parity_enc<DC>(sgn, w) ^ (neg ? 1u : 0u);
         return qkds::pack_iv(neg_iv_if(sigma != 0u, m));
     };
     uint2 wa = plan_word(prs, t, lane);
@@ -478,7 +508,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         wa = wc;
     }
     ms.st_w(pend, pv);
-    if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
+    if (bad != 0 && lane == 0) atomicOr(round_word, 2u);
 }
 
 // The same check phase with the input bound of the NEXT task's edge and the
@@ -500,7 +530,8 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
     int t = wave;
     if (t >= n_tasks) return;
     const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
-    bool bad = false;
+    // lanes that could not certify (wave masks: scalar ors, no per-lane flag)
+    uint64_t bad = 0;
     if (lane < DC) row[64 + lane] = 0.0;
     auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
     // |b2c| of an edge, its sign and whether the interval certifies it
@@ -509,8 +540,11 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         const f2 bv = qkds::unpack_iv(xv);
         neg = bv.y < 0.0f;
         ab = neg_iv_if(neg, bv);
-        const bool ok = (neg || bv.x > 0.0f) && ab.x > 1.0e-30f;
-        bad |= !ok && pw_slot(w) != dummy;
+        // certified: the interval excludes 0 by a margin ((neg || lo > 0) &&
+        // |.|lo > 1e-30, of which the second alone decides: |.|lo is -hi
+        // when neg, lo otherwise; NaN fails either way)
+        const bool ok = ab.x > 1.0e-30f;
+        bad |= __ballot(!ok && pw_slot(w) != dummy);
         return ok;
     };
     // (the plan has kPlanPadTasks idle tasks past n_tasks: loads ahead need no test)
@@ -540,23 +574,20 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         const bool ok_n = input(ms.pick(x_n), w_n, neg_n, ab_n);
         // this task's extrinsic sums (as spec_check_phase_psi)
         wave_lds_sync();
-        const int start = pw_start(w_t);
-        const int deg = pw_deg(w_t);
-        const f2 sum = seg_sum<DC>(row, start, SegWeights<DC>(wtab, deg, lane - start));
+        const int start = seg_start(w_t);
+        const int deg = seg_deg<DC>(w_t);
+        const f2 sum = seg_sum<DC>(row, start, seg_weights<DC>(wtab, w_t, lane));
         const float nr = DC <= 8 ? (float)(DC + 2) : (float)(deg + 2);
         const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
         f2 ext = sum + f2{-mg, mg};
         ext.x = ext.x > 0.0f ? ext.x : 0.0f;
-        bad |= !(ext.y < qkds::kPsiSumMax);
+        bad |= __ballot(!(ext.y < qkds::kPsiSumMax));
         f2 ph_n, m;
         qkds::phi_pair(ab_n.x, ab_n.y, ext.x, ext.y, ph_n, m);
         // this task's c2b: threshold_matrix (:246-249) on the magnitude, the sign
         m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
         m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
-        const uint32_t j = pw_chk(w_t);
-        const uint32_t sj = (tsyn[j >> 5] >> (j & 31)) & 1u;
-        const uint32_t sigma =
-            sj ^ (uint32_t)(DC < 32 ? seg_parity32(sgn_t, w_t) : seg_parity(sgn_t, w_t)) ^ (neg_t ? 1u : 0u);
+        const uint32_t sigma = seg_sbit(w_t) ^ seg_parity_enc<DC>(sgn_t, w_t) ^ (neg_t ? 1u : 0u);
         ms.st_w(slot(w_t), qkds::pack_iv(neg_iv_if(sigma != 0u, m)));
         // the next task's input bounds into the row
         row[lane] = qkds::pack_iv(ok_n ? ph_n : f2{0.0f, 0.0f});
@@ -573,7 +604,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         if (!step(wnn, wd, wt, wn, xa, xb)) break;
         if (!step(wd, wt, wn, wnn, xb, xa)) break;
     }
-    if (__any(bad) && lane == 0) atomicOr(round_word, 2u);
+    if (bad != 0 && lane == 0) atomicOr(round_word, 2u);
 }
 
 // The folded first iteration as a table (speculative kernel, QKD path): its

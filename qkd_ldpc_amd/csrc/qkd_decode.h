@@ -539,6 +539,23 @@ __host__ __device__ inline uint32_t encode_slot(uint32_t x, uint32_t S, uint32_t
     return x < S ? (kSlotLds | (msg + x * esz)) : (kSlotGlobalBase + (x - S) * esz);
 }
 
+// The encoded plan's second word (check-degree bucket DC), the lane's
+// segment and its check's target bit pre-decoded for the check phases:
+//   bits 0-4    j & 31: the target bit's position in its syndrome word (a
+//               shift by the whole word uses these bits only)
+//   bits 5-10   start: the segment's first lane
+//   bits 11-18  wi: DC <= 16: (deg - 1) * DC + min(lane - start, DC - 1), the
+//               row of the segment-weight table (SegWeights); wider buckets: deg - 1
+//   bits 19-31  (j >> 5) * 4: the byte offset of the check's syndrome word
+// (needs M <= 65536: the split decoder's limit).
+constexpr uint32_t kSegStartShift = 5, kSegWiShift = 11, kSegWordShift = 19;
+constexpr int32_t kMaxChecksSplit = 65536;
+__host__ __device__ inline uint32_t encode_seg(uint32_t j, uint32_t start, uint32_t deg, uint32_t lane, uint32_t dc) {
+    const uint32_t p = lane - start;
+    const uint32_t wi = dc <= 16 ? (deg - 1) * dc + (p < dc - 1 ? p : dc - 1) : deg - 1;
+    return (j & 31u) | (start << kSegStartShift) | (wi << kSegWiShift) | (((j >> 5) * 4u) << kSegWordShift);
+}
+
 using DecodeFn = void (*)(DecodeArgs);
 // decode_split.hip: the split-store kernel for (mode, rule in {kRuleSp64,
 // kRuleSp32}, clamp, check-degree bucket); *dc receives the bucket.
