@@ -101,9 +101,27 @@ __device__ __forceinline__ uint32_t seg_parity_enc(uint64_t ballot, uint2 w) {
 // row[start + k] times its weight (0 or 1, exact), in ascending order (a
 // pairwise tree, depth ~log2(DC) for two more operations, measured no faster:
 // DESIGN.md §4.3). The caller charges its rounding relative to the sum.
+#ifndef QKD_SEG_BATCH
+#define QKD_SEG_BATCH 1
+#endif
 template <int DC>
 __device__ __forceinline__ qkds::f2 seg_sum(const double* row, int start, const SegWeights<DC>& wk) {
     qkds::f2 sum = qkds::f2{0.0f, 0.0f};
+    if constexpr (QKD_SEG_BATCH && DC <= 8) {
+        // every row entry and weight read before the first use (a scheduling
+        // barrier: left alone, the scheduler reuses registers and serialises
+        // the reads into DC / 2 LDS round trips)
+        qkds::f2 v[DC];
+        float w[DC];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) v[k] = qkds::unpack_iv(row[start + k]);
+#pragma unroll
+        for (int k = 0; k < DC; ++k) w[k] = wk[k];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < DC; ++k) sum = __builtin_elementwise_fma(v[k], qkds::f2(w[k]), sum);
+        return sum;
+    }
 #pragma unroll
     for (int k = 0; k < DC; ++k) sum = __builtin_elementwise_fma(qkds::unpack_iv(row[start + k]), qkds::f2(wk[k]), sum);
     return sum;
@@ -431,7 +449,10 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
 // round. Two forms: spec_check_phase_paired (below) for b2c intervals, and
 // this one for the iteration after the folded first one, whose slots hold
 // the psi bounds of exact b2c already (psi_of_exact, spec_bit_phase), so only
-// the output bound is evaluated per edge. Pipelined as split_check_phase.
+// the output bound is evaluated per edge. Pipelined as
+// spec_check_phase_paired: each task's row (its psi bounds) is written at the
+// end of the task before, from its slot loaded a task earlier still, so the
+// row reads of a task follow its start with no LDS write in between.
 template <int DC>
 __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ plan, const uint32_t* tsyn,
                                                  const SplitStore<double>& ms, double* row, const float* wtab,
@@ -449,24 +470,38 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
     // there: keep them finite (the prologue stages key words in this region)
     if (lane < DC) row[64 + lane] = 0.0;
     auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
-    auto edge = [&](double xv, uint2 w) -> double {
-        // phi(|b2c|) / ln 2 with the sign of b2c in the low word, NaN when
-        // the sign is not certain (psi_of_exact); idle lanes (the dummy
-        // column) do not count
+    // phi(|b2c|) / ln 2 with the sign of b2c in the low word, NaN when the
+    // sign is not certain (psi_of_exact); idle lanes (the dummy column) do
+    // not count. The row entry is the magnitude's bounds (0 when uncertain).
+    auto input = [&](double xv, uint2 w, bool& neg) -> f2 {
         const f2 bv = qkds::unpack_iv(xv);
-        const bool neg = bv.x < 0.0f;
+        neg = bv.x < 0.0f;
         const bool ok = bv.x == bv.x;
         bad |= __ballot(!ok && pw_slot(w) != dummy);
-        const f2 ph = ok ? neg_iv_if(neg, bv) : f2{0.0f, 0.0f};
-        row[lane] = qkds::pack_iv(ph);
-        const uint64_t sgn = __ballot(neg);
+        return ok ? neg_iv_if(neg, bv) : f2{0.0f, 0.0f};
+    };
+    uint2 wt = plan_word(prs, t, lane);
+    uint2 wn = plan_word(prs, t + NW, lane);
+    uint2 wnn = plan_word(prs, t + 2 * NW, lane);
+    bool neg_t;
+    row[lane] = qkds::pack_iv(input(ms.ld_w(slot(wt)), wt, neg_t));
+    uint64_t sgn_t = __ballot(neg_t);
+    uint32_t sb_t = seg_sbit(wt);
+    using Raw = SplitStore<double>::Raw;
+    // One task (as spec_check_phase_paired's step): task t's c2b from the row,
+    // then task t + NW's row entry from its slot (loaded a task earlier).
+    auto step = [&](const uint2 w_t, const uint2 w_n, const uint2 w_nn, uint2& w_ld, const Raw& x_n,
+                    Raw& x_ld) -> bool {
+        w_ld = plan_word(prs, t + 3 * NW, lane);
+        x_ld = ms.ld_raw(slot(w_nn));
+        const uint32_t sb_n = seg_sbit(w_n);
+        bool neg_n;
+        const f2 ph_n = input(ms.pick(x_n), w_n, neg_n);
         wave_lds_sync();
-        const int start = seg_start(w);
-        const int deg = seg_deg<DC>(w);
+        const int deg = seg_deg<DC>(w_t);
         // extrinsic sum over the other lanes of the segment (a subtraction of
         // the own term would widen the interval by the own term's width)
-        // (weight of entry k: bit k of the segment's mask without this lane)
-        const f2 sum = seg_sum<DC>(row, start, seg_weights<DC>(wtab, w, lane));
+        const f2 sum = seg_sum<DC>(row, seg_start(w_t), seg_weights<DC>(wtab, w_t, lane));
         // widened by the binary32 roundings (relative to the sum; small
         // buckets charge every segment the bucket's count) and the
         // reference's binary64 roundings (absolute, qkd_spec.h)
@@ -481,33 +516,23 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         // canonicalisation fminf needs for a kernel argument)
         m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
         m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
-        const uint32_t sigma = seg_sbit(w) ^ seg_parity_enc<DC>(sgn, w) ^ (neg ? 1u : 0u);
-        return qkds::pack_iv(neg_iv_if(sigma != 0u, m));
+        const uint32_t sigma = sb_t ^ seg_parity_enc<DC>(sgn_t, w_t) ^ (neg_t ? 1u : 0u);
+        ms.st_w(slot(w_t), qkds::pack_iv(neg_iv_if(sigma != 0u, m)));
+        row[lane] = qkds::pack_iv(ph_n);
+        sgn_t = __ballot(neg_n);
+        neg_t = neg_n;
+        sb_t = sb_n;
+        t += NW;
+        return t < n_tasks;
     };
-    uint2 wa = plan_word(prs, t, lane);
-    uint2 wb = plan_word(prs, t + NW, lane);
-    auto xa = ms.ld_raw(slot(wa));
-    uint32_t pend = 0xffffffffu;
-    double pv = 0;
+    Raw xa = ms.ld_raw(slot(wn)), xb;
+    uint2 wd;
     for (;;) {
-        if (pend != 0xffffffffu) ms.st_w(pend, pv);
-        const uint2 wc = plan_word(prs, t + 2 * NW, lane);
-        const auto xb = ms.ld_raw(slot(wb));
-        pv = edge(ms.pick(xa), wa);
-        pend = slot(wa);
-        t += NW;
-        if (t >= n_tasks) break;
-        ms.st_w(pend, pv);
-        wa = plan_word(prs, t + 2 * NW, lane);
-        xa = ms.ld_raw(slot(wc));
-        pv = edge(ms.pick(xb), wb);
-        pend = slot(wb);
-        t += NW;
-        if (t >= n_tasks) break;
-        wb = wa;
-        wa = wc;
+        if (!step(wt, wn, wnn, wd, xa, xb)) break;
+        if (!step(wn, wnn, wd, wt, xb, xa)) break;
+        if (!step(wnn, wd, wt, wn, xa, xb)) break;
+        if (!step(wd, wt, wn, wnn, xb, xa)) break;
     }
-    ms.st_w(pend, pv);
     if (bad != 0 && lane == 0) atomicOr(round_word, 2u);
 }
 
@@ -558,6 +583,9 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         row[lane] = qkds::pack_iv(ok ? qkds::phi_bounds(ab.x, ab.y) : f2{0.0f, 0.0f});
     }
     uint64_t sgn_t = __ballot(neg_t);
+    // the target bit of a task's check is read one task ahead (its LDS round
+    // trip then shares the wait of the row reads)
+    uint32_t sb_t = seg_sbit(wt);
     using Raw = SplitStore<double>::Raw;
     // One task: task t's c2b from the row and the input bound of task t + NW
     // (its slot x_n, loaded one task earlier) into the row; loads the plan
@@ -569,6 +597,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
                     Raw& x_ld) -> bool {
         w_ld = plan_word(prs, t + 3 * NW, lane);
         x_ld = ms.ld_raw(slot(w_nn));
+        const uint32_t sb_n = seg_sbit(w_n);
         bool neg_n;
         f2 ab_n;
         const bool ok_n = input(ms.pick(x_n), w_n, neg_n, ab_n);
@@ -587,12 +616,13 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         // this task's c2b: threshold_matrix (:246-249) on the magnitude, the sign
         m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
         m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
-        const uint32_t sigma = seg_sbit(w_t) ^ seg_parity_enc<DC>(sgn_t, w_t) ^ (neg_t ? 1u : 0u);
+        const uint32_t sigma = sb_t ^ seg_parity_enc<DC>(sgn_t, w_t) ^ (neg_t ? 1u : 0u);
         ms.st_w(slot(w_t), qkds::pack_iv(neg_iv_if(sigma != 0u, m)));
         // the next task's input bounds into the row
         row[lane] = qkds::pack_iv(ok_n ? ph_n : f2{0.0f, 0.0f});
         sgn_t = __ballot(neg_n);
         neg_t = neg_n;
+        sb_t = sb_n;
         t += NW;
         return t < n_tasks;
     };
