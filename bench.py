@@ -382,7 +382,7 @@ def main():
     L = Q._native.lib()
     sptr = int(stream.cuda_stream)
 
-    def step(ev=None, variant=args.variant):
+    def step(ev=None, variant=args.variant, reduce=True):
         flags = Q.decoder_flags(True, **VARIANTS[variant])
         if ev is not None:
             ev[0].record(stream)
@@ -393,7 +393,7 @@ def main():
             ev[1].record(stream)
         Q._native.check(L.qkd_counters_batch(iters.data_ptr(), sp.data_ptr(), ko.data_ptr(), F,
                                              counters.data_ptr(), H.device, sptr))
-        if world > 1:
+        if world > 1 and reduce:
             allreduce_counters(counters)
 
     Q.spec_replays(ws, reset=True)
@@ -402,11 +402,14 @@ def main():
     # warmup steps of a 2 ms step take: untimed steps fill --prewarm-ms first,
     # so the K timed steps see steady-state clocks, as a QKD post-processing
     # pipeline running continuously does. Then the W warmup steps proper.
+    # (Timed by each rank's own clock, so ranks run different numbers of
+    # prewarm steps: those skip the counter all-reduce, which every rank must
+    # enter equally often.)
     prewarm_steps = 0
     t_pw = time.perf_counter()
     while (time.perf_counter() - t_pw) * 1e3 < args.prewarm_ms:
         for _ in range(5):
-            step()
+            step(reduce=False)
         prewarm_steps += 5
         torch.cuda.synchronize()
     for _ in range(args.warmup):

@@ -714,6 +714,12 @@ __global__ void keygen_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n
 // writer of each low position is found with an LDS atomicMax. A Lemire rejection
 // (probability ~ range / 2^64 per draw) shifts every later draw: such a frame
 // is regenerated serially by its lane 0 from its seed.
+// R32 (N <= 65536): every pair's range (i + 1)(i + 2) < 2^32, so the Lemire
+// products are 64 x 32 bits and the pair split x / (i + 2) a binary32
+// reciprocal product with one exact integer correction (the lanes of a frame
+// diverge between Alice's bits and the shuffle draws, so the wave pays both
+// paths on every draw: the binary64 division was most of it).
+template <bool R32>
 __global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
                                                          uint32_t words, uint32_t ne, uint32_t chunk,
                                                          uint32_t n_frames, const uint64_t* __restrict__ jump,
@@ -787,15 +793,36 @@ __global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_
             const uint32_t i = i0 + 2u * (uint32_t)(d - pair0);
             const uint64_t b1 = (uint64_t)i + 2;
             const uint64_t range = ((uint64_t)i + 1) * b1;
-            const uint64_t lo = r * range;
-            if (lo < range && lo < (0 - range) % range) s_reject[slot] = 1;
-            const uint64_t x = qkdr::mul_hi64(r, range);
-            // quotient through binary64, corrected to the exact integer one
-            uint64_t a = (uint64_t)((double)x / (double)b1);
-            if (a * b1 > x) --a;
-            else if (x - a * b1 >= b1) ++a;
-            const uint32_t qa = (uint32_t)a;
-            const uint32_t qb = (uint32_t)(x - a * b1);
+            uint32_t qa, qb;
+            if constexpr (R32) {
+                // r * range = p1 * 2^32 + p0 with range < 2^32: the low 64 bits
+                // (Lemire's test) and the high ones (x < range < 2^32)
+                const uint32_t rg = (uint32_t)range, bb = (uint32_t)b1;
+                const uint64_t p0 = (uint64_t)(uint32_t)r * rg;
+                const uint64_t p1 = (uint64_t)(uint32_t)(r >> 32) * rg;
+                const uint64_t lo = p0 + (p1 << 32);
+                if (lo < range) {
+                    if (lo < (0 - range) % range) s_reject[slot] = 1;
+                }
+                const uint32_t x = (uint32_t)((p1 + (p0 >> 32)) >> 32);
+                // x / bb < 2^16 to 2^-21 relative: off by at most one
+                uint32_t q = (uint32_t)((float)x * __builtin_amdgcn_rcpf((float)bb));
+                int32_t rem = (int32_t)(x - q * bb);
+                if (rem < 0) { --q; rem += (int32_t)bb; }
+                else if (rem >= (int32_t)bb) { ++q; rem -= (int32_t)bb; }
+                qa = q;
+                qb = (uint32_t)rem;
+            } else {
+                const uint64_t lo = r * range;
+                if (lo < range && lo < (0 - range) % range) s_reject[slot] = 1;
+                const uint64_t x = qkdr::mul_hi64(r, range);
+                // quotient through binary64, corrected to the exact integer one
+                uint64_t a = (uint64_t)((double)x / (double)b1);
+                if (a * b1 > x) --a;
+                else if (x - a * b1 >= b1) ++a;
+                qa = (uint32_t)a;
+                qb = (uint32_t)(x - a * b1);
+            }
             if (i < ne) {
                 park[(i - i0) >> 1] = make_uint2(qa, qb);
             } else {
@@ -1632,7 +1659,8 @@ static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uin
     // (the fast kernel's per-frame LDS times kKeygenFrames must fit a workgroup's LDS)
     const size_t lds = (size_t)kKeygenFrames * (2 * (size_t)ne * sizeof(uint32_t) + (ne / 2 + 1) * sizeof(uint2));
     if (ne <= kKeygenFastMaxErrors && c->d_jump && !serial && lds <= kLdsBytesMax) {
-        hipLaunchKernelGGL(keygen_fast_kernel, dim3((unsigned)((n_frames + kKeygenFrames - 1) / kKeygenFrames)),
+        auto* const kg = c->n <= 65536 ? keygen_fast_kernel<true> : keygen_fast_kernel<false>;
+        hipLaunchKernelGGL(kg, dim3((unsigned)((n_frames + kKeygenFrames - 1) / kKeygenFrames)),
                            dim3(kKeygenBlock), lds, stream, seeds, offset, (uint32_t)c->n, words, (uint32_t)ne,
                            c->keygen_chunk, (uint32_t)n_frames, c->d_jump, matrix ? nullptr : c->d_jpoly,
                            ws->alice_w, ws->bob_w, exact_q, replay);
