@@ -879,6 +879,171 @@ __global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_
     }
 }
 
+// The same key pair by two waves per frame (the default generator): in the
+// one-wave form every lane's chunk mixes Alice's bits and shuffle draws, so
+// the wave runs both loop bodies on every draw. Here wave 0's 64 lanes draw
+// only Alice's bits (lane l: draws [l * cb, (l + 1) * cb), OR-ed into LDS
+// words, as chunks need not end on word boundaries) and wave 1's only the
+// shuffle's (lane l: from draw N + l * cs): each lane jumps once (its own
+// polynomial, c->d_jpoly2), every loop is uniform, and a frame has twice the
+// waves to hide its chains behind. The shuffle's low steps are replayed and
+// the last writers found exactly as in keygen_fast_kernel; the flips land in
+// an LDS copy of the key, and both keys leave as whole coalesced words.
+// LDS: low[ne], last[ne], park[ne / 2 + 1], alice[words], bob[words].
+template <bool R32>
+__global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
+                                                           uint32_t words, uint32_t ne, uint32_t cb, uint32_t cs,
+                                                           const uint64_t* __restrict__ jpoly, uint64_t* alice_w,
+                                                           uint64_t* bob_w, double* exact_q, uint32_t force_serial) {
+    extern __shared__ uint64_t ks_lds[];
+    __shared__ uint32_t s_lone, s_reject;
+    uint32_t* low = reinterpret_cast<uint32_t*>(ks_lds);
+    uint32_t* last = low + ne;
+    uint2* park = reinterpret_cast<uint2*>(last + ne);        // 8-byte aligned: 2 ne words before it
+    uint64_t* aw = reinterpret_cast<uint64_t*>(park + ne / 2 + 1);
+    uint64_t* bw = aw + words;
+    const uint32_t f = blockIdx.x;                              // one frame per workgroup, grid = frames
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const bool shuffle_wave = tid >= 64;                        // wave-uniform
+    const bool even = (n & 1u) == 0;
+    const uint64_t pair0 = even ? (uint64_t)n + 1 : (uint64_t)n;
+    const uint32_t i0 = even ? 2u : 1u;
+    const uint64_t draws = qkdr::trial_draws(n);
+
+    qkdr::Xoshiro256pp g;
+    g.seed(seeds[f] + offset);
+    {
+        uint64_t st[4] = {g.s0, g.s1, g.s2, g.s3};
+        const uint64_t p[4] = {jpoly[tid * 4 + 0], jpoly[tid * 4 + 1], jpoly[tid * 4 + 2], jpoly[tid * 4 + 3]};
+        qkdr::jump_poly_apply(p, st);
+        g.s0 = st[0]; g.s1 = st[1]; g.s2 = st[2]; g.s3 = st[3];
+    }
+    for (uint32_t q = tid; q < ne; q += 128) {
+        low[q] = q;
+        last[q] = 0;
+    }
+    for (uint32_t w = tid; w < words; w += 128) aw[w] = 0;
+    if (tid == 0) {
+        s_lone = 0;
+        s_reject = force_serial;
+    }
+    __syncthreads();
+
+    if (!shuffle_wave) {
+        const uint32_t first = lane * cb;
+        const uint32_t end = min(first + cb, n);
+        uint64_t acc = 0;
+        for (uint32_t d = first; d < end; ++d) {
+            acc |= (g.next() >> 63) << (d & 63u);
+            if ((d & 63u) == 63u || d + 1 == end) {
+                atomicOr(reinterpret_cast<unsigned long long*>(&aw[d >> 6]), (unsigned long long)acc);
+                acc = 0;
+            }
+        }
+    } else {
+        const uint64_t first = (uint64_t)n + (uint64_t)lane * cs;
+        const uint64_t end = min(first + cs, draws);
+        for (uint64_t d = first; d < end; ++d) {
+            const uint64_t r = g.next();
+            if (d < pair0) {
+                s_lone = (uint32_t)(r >> 63);
+                continue;
+            }
+            const uint32_t i = i0 + 2u * (uint32_t)(d - pair0);
+            const uint64_t b1 = (uint64_t)i + 2;
+            const uint64_t range = ((uint64_t)i + 1) * b1;
+            uint32_t qa, qb;
+            if constexpr (R32) {
+                // (keygen_fast_kernel's 32-bit form)
+                const uint32_t rg = (uint32_t)range, bb = (uint32_t)b1;
+                const uint64_t p0 = (uint64_t)(uint32_t)r * rg;
+                const uint64_t p1 = (uint64_t)(uint32_t)(r >> 32) * rg;
+                const uint64_t lo = p0 + (p1 << 32);
+                if (lo < range) {
+                    if (lo < (0 - range) % range) s_reject = 1;
+                }
+                const uint32_t x = (uint32_t)((p1 + (p0 >> 32)) >> 32);
+                uint32_t q = (uint32_t)((float)x * __builtin_amdgcn_rcpf((float)bb));
+                int32_t rem = (int32_t)(x - q * bb);
+                if (rem < 0) { --q; rem += (int32_t)bb; }
+                else if (rem >= (int32_t)bb) { ++q; rem -= (int32_t)bb; }
+                qa = q;
+                qb = (uint32_t)rem;
+            } else {
+                const uint64_t lo = r * range;
+                if (lo < range && lo < (0 - range) % range) s_reject = 1;
+                const uint64_t x = qkdr::mul_hi64(r, range);
+                uint64_t a = (uint64_t)((double)x / (double)b1);
+                if (a * b1 > x) --a;
+                else if (x - a * b1 >= b1) ++a;
+                qa = (uint32_t)a;
+                qb = (uint32_t)(x - a * b1);
+            }
+            if (i < ne) {
+                park[(i - i0) >> 1] = make_uint2(qa, qb);
+            } else {
+                if (qa < ne) atomicMax(&last[qa], i);
+                if (qb < ne) atomicMax(&last[qb], i + 1);
+            }
+        }
+    }
+    __syncthreads();
+
+    uint64_t* A = alice_w + (size_t)f * words;
+    uint64_t* B = bob_w + (size_t)f * words;
+    if (s_reject) {
+        // exact serial regeneration of this frame (never observed in practice)
+        if (tid == 0) {
+            qkdr::Xoshiro256pp h;
+            h.seed(seeds[f] + offset);
+            for (uint32_t w = 0; w < words; ++w) {
+                const uint32_t nb = min(64u, n - w * 64);
+                uint64_t v = 0;
+                for (uint32_t b = 0; b < nb; ++b) v |= (h.next() >> 63) << b;
+                A[w] = v;
+                B[w] = v;
+            }
+            qkdr::shuffle_low_positions(h, n, ne, low);
+            for (uint32_t q = 0; q < ne; ++q) B[low[q] >> 6] ^= 1ull << (low[q] & 63);
+            if (exact_q) exact_q[f] = (double)ne / (double)n;
+        }
+        return;                                                // (workgroup-uniform)
+    }
+    if (tid == 64) {
+        // replay of the steps with index < ne (shuffle_low_positions' step())
+        auto step = [&](uint32_t si, uint32_t x) {
+            if (si < ne) {
+                const uint32_t v = low[x];
+                low[x] = si;
+                low[si] = v;
+            } else if (x < ne) {
+                low[x] = si;
+            }
+        };
+        if (n > 1) {
+            if (even) step(1, s_lone);
+            for (uint32_t i = i0; i < ne && i < n; i += 2) {
+                const uint2 q = park[(i - i0) >> 1];
+                step(i, q.x);
+                step(i + 1, q.y);
+            }
+        }
+        if (exact_q) exact_q[f] = (double)ne / (double)n;
+    }
+    for (uint32_t w = tid; w < words; w += 128) bw[w] = aw[w];
+    __syncthreads();
+    for (uint32_t q = tid; q < ne; q += 128) {
+        const uint32_t pos = last[q] ? last[q] : low[q];
+        atomicXor(reinterpret_cast<unsigned long long*>(&bw[pos >> 6]), 1ull << (pos & 63u));
+    }
+    __syncthreads();
+    for (uint32_t w = tid; w < words; w += 128) {
+        A[w] = aw[w];
+        B[w] = bw[w];
+    }
+}
+
 // ---- batch reduction (simulation.cpp:252-312) ----------------------------------
 __global__ void counters_kernel(const uint32_t* iters, const uint8_t* sp, const uint8_t* ko,
                                 uint32_t n_frames, qkd_counters* out) {
@@ -1649,13 +1814,24 @@ static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uin
     if (s != QKD_OK) return s;
     const uint32_t words = (uint32_t)((c->n + 63) / 64);
     // QKD_KEYGEN=serial forces the one-thread-per-frame kernel, QKD_KEYGEN=replay
-    // the fast kernel's in-wave serial path for every frame, QKD_KEYGEN=matrix
-    // the fast kernel with its lane jumps as GF(2) matrix products instead of
-    // polynomials (tests of all three).
+    // the two-wave kernel's serial path for every frame, QKD_KEYGEN=lanes the
+    // one-wave kernel (keygen_fast_kernel), QKD_KEYGEN=matrix that kernel with its
+    // lane jumps as GF(2) matrix products instead of polynomials (tests of all).
     const char* mode = getenv("QKD_KEYGEN");
     const bool serial = mode && !strcmp(mode, "serial");
     const uint32_t replay = mode && !strcmp(mode, "replay") ? 1u : 0u;
     const bool matrix = mode && !strcmp(mode, "matrix");
+    const bool lanes = mode && !strcmp(mode, "lanes");
+    // the two-wave generator (default; QKD_KEYGEN=replay forces its serial path)
+    const size_t lds2 = (2 * (size_t)ne + 2 * (ne / 2 + 1)) * sizeof(uint32_t) + 2 * (size_t)words * sizeof(uint64_t);
+    if (ne <= kKeygenFastMaxErrors && c->d_jpoly2 && !serial && !matrix && !lanes && lds2 <= kLdsBytesMax) {
+        auto* const kg = c->n <= 65536 ? keygen_split_kernel<true> : keygen_split_kernel<false>;
+        hipLaunchKernelGGL(kg, dim3((unsigned)n_frames), dim3(128), lds2, stream, seeds, offset, (uint32_t)c->n,
+                           words, (uint32_t)ne, c->kg_cb, c->kg_cs, c->d_jpoly2, ws->alice_w, ws->bob_w, exact_q,
+                           replay);
+        QKD_HIP(hipGetLastError());
+        return QKD_OK;
+    }
     // (the fast kernel's per-frame LDS times kKeygenFrames must fit a workgroup's LDS)
     const size_t lds = (size_t)kKeygenFrames * (2 * (size_t)ne * sizeof(uint32_t) + (ne / 2 + 1) * sizeof(uint2));
     if (ne <= kKeygenFastMaxErrors && c->d_jump && !serial && lds <= kLdsBytesMax) {

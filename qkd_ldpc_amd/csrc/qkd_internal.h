@@ -166,6 +166,11 @@ struct qkd_code {
     uint64_t* d_jump = nullptr;
     // the same jumps as polynomials: d_jpoly[l] = x^(l * chunk) mod P (4 words)
     uint64_t* d_jpoly = nullptr;
+    // keygen_split_kernel (the default): wave 0's lane l draws Alice's bits
+    // [l * kg_cb, (l + 1) * kg_cb), wave 1's lane l the shuffle draws from
+    // N + l * kg_cs; d_jpoly2[w * 64 + l] = x^(start) mod P
+    uint32_t kg_cb = 0, kg_cs = 0;
+    uint64_t* d_jpoly2 = nullptr;
     int cu_count = 0;
     qkd_workspace* default_ws = nullptr;
 

@@ -294,6 +294,20 @@ inline void poly_mulmod(const uint64_t a[4], const uint64_t b[4], const uint64_t
     for (int w = 0; w < 4; ++w) r[w] = acc[w];
 }
 
+// r = x^k mod P (square and multiply).
+inline void poly_x_pow(uint64_t k, const uint64_t P[4], uint64_t r[4]) {
+    uint64_t acc[4] = {1, 0, 0, 0}, base[4] = {2, 0, 0, 0}, t[4];
+    for (; k; k >>= 1) {
+        if (k & 1u) {
+            poly_mulmod(acc, base, P, t);
+            for (int w = 0; w < 4; ++w) acc[w] = t[w];
+        }
+        poly_mulmod(base, base, P, t);
+        for (int w = 0; w < 4; ++w) base[w] = t[w];
+    }
+    for (int w = 0; w < 4; ++w) r[w] = acc[w];
+}
+
 // out[l] = x^(l * chunk) mod P for lanes l = 0 .. lanes-1 (4 words each).
 inline bool xoshiro_jump_polys(uint64_t chunk, int lanes, uint64_t* out) {
     uint64_t P[4];

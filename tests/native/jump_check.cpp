@@ -42,6 +42,25 @@ int main() {
             }
         }
     }
+    // x^k mod P by square and multiply (the two-wave generator's starts,
+    // keygen_split_kernel): the same states as stepping k draws
+    {
+        uint64_t P[4];
+        if (!qkdr::xoshiro_charpoly(P)) bad += 1000;
+        for (uint64_t k : {0ull, 1ull, 2ull, 63ull, 160ull, 10241ull, 10240ull + 63ull * 81ull}) {
+            uint64_t p[4];
+            qkdr::poly_x_pow(k, P, p);
+            for (uint64_t seed : {0ull, 777ull}) {
+                qkdr::Xoshiro256pp g, h;
+                g.seed(seed);
+                h.seed(seed);
+                uint64_t s[4] = {g.s0, g.s1, g.s2, g.s3};
+                qkdr::jump_poly_apply(p, s);
+                for (uint64_t j = 0; j < k; ++j) h.next();
+                if (s[0] != h.s0 || s[1] != h.s1 || s[2] != h.s2 || s[3] != h.s3) bad++;
+            }
+        }
+    }
     // the generator's published jump(): JUMP = x^(2^128) mod P
     {
         uint64_t P[4], r[4] = {2, 0, 0, 0};          // x

@@ -343,11 +343,12 @@ def test_device_math_bit_exact_vs_glibc(Q, oracle_mod, which):
     assert bad.size == 0, [(float.hex(x[i]), float.hex(got[i]), float.hex(want[i])) for i in bad[:5]]
 
 
-@pytest.mark.parametrize("mode", ["fast", "matrix", "replay", "serial"])
+@pytest.mark.parametrize("mode", ["fast", "lanes", "matrix", "replay", "serial"])
 def test_keygen_kernels_agree_with_oracle(Q, oracle_mod, monkeypatch, mode):
-    """The wave-per-frame jump-ahead generator (default), its in-wave serial
-    regeneration (taken after a Lemire rejection; forced here) and the
-    one-thread-per-frame kernel all reproduce run_trial's keys."""
+    """The two-wave jump-ahead generator (default), its serial regeneration
+    (taken after a Lemire rejection; forced here), the one-wave generator with
+    polynomial and matrix jumps, and the one-thread-per-frame kernel all
+    reproduce run_trial's keys."""
     if mode != "fast":
         monkeypatch.setenv("QKD_KEYGEN", mode)
     rng = np.random.default_rng(31)
