@@ -21,16 +21,22 @@ N_XCD = 8
 
 
 def collect(dirs):
+    """Counter values per kernel and counter, and per kernel and counter the
+    dispatch durations (ns, End - Start of the same dispatch rows)."""
     per = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in dirs:
         for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
             per[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return per
+            if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+                dur[r["Kernel_Name"]][r["Counter_Name"]].append(
+                    float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+    return per, dur
 
 
 def main():
     out_path, summary, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
-    per = collect(dirs)
+    per, dur = collect(dirs)
     want = os.environ.get("QKD_PMC_KERNEL")
     names = [k for k in per if (want in k if want else "decode" in k)]
     assert len(names) == 1, names
@@ -49,7 +55,17 @@ def main():
     if "GRBM_GUI_ACTIVE" in c:
         cyc = c["GRBM_GUI_ACTIVE"] / N_XCD          # summed over the 8 XCDs
         v["gpu_cycles"] = cyc
-        v["effective_clock_ghz"] = cyc / t / 1e9
+        # the clock over the counted dispatches' own durations (the PMC pass runs
+        # the kernel under other conditions than the trace pass's warm average)
+        g = per[names[0]]["GRBM_GUI_ACTIVE"]
+        d = dur[names[0]].get("GRBM_GUI_ACTIVE", [])
+        if len(d) == len(g) and d and min(d) > 0:
+            v["effective_clock_ghz"] = sum(x / N_XCD / y for x, y in zip(g, d)) / len(g)
+            v["pmc_pass_kernel_ms"] = sum(d) / len(d) / 1e6
+            v["clock_source"] = "GRBM_GUI_ACTIVE / 8 over each counted dispatch's End - Start"
+        else:
+            v["effective_clock_ghz"] = cyc / t / 1e9
+            v["clock_source"] = "GRBM_GUI_ACTIVE / 8 over the trace pass's warm average"
         if "SQ_INSTS_VALU" in c:
             v["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
             v["valu_issue_util_2cyc"] = c["SQ_INSTS_VALU"] * 2 / (cyc * N_SIMD)
@@ -63,7 +79,7 @@ def main():
         v["wait_lds_frac"] = c["SQ_WAIT_INST_LDS"] / c["SQ_WAVE_CYCLES"]
     if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
         v["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
-    v["formulas"] = ("effective clock = GRBM_GUI_ACTIVE/8 / t; valu_issue_util_2cyc = SQ_INSTS_VALU x 2 "
+    v["formulas"] = ("effective clock: clock_source; valu_issue_util_2cyc = SQ_INSTS_VALU x 2 "
                      "cycles (wave64 over 32 lanes) / (cycles x 1024 SIMDs), binary64 ops take longer; "
                      "valu_active_util_x4 = SQ_ACTIVE_INST_VALU x 4 / (cycles x 1024); lds_conflict_frac = "
                      "SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES")
