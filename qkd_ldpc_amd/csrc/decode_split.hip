@@ -32,6 +32,8 @@
 // the second check phase looks it up.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "qkd_decode.h"
 #include "qkd_spec.h"
 
@@ -706,34 +708,65 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                                                uint32_t f, int tid, int wave, int lane) {
     using qkds::f2;
     static_assert(!DV3 || kDvUnroll == 3, "DV3 unrolls three rows");
-    const uint32_t n_pad = (uint32_t)c.n_pad;
+    // the code's sizes as scalars (read through the DecodeArgs reference they
+    // are not known to be uniform, and every row's LDS / global choice, k *
+    // n_pad + iw < S, then compiles to a divergent branch)
+    const uint32_t n_pad = __builtin_amdgcn_readfirstlane((uint32_t)c.n_pad);
+    const int cn = __builtin_amdgcn_readfirstlane(c.n);
     const double llr_p = a.log_p;
+    // Fixed rows (FX): row 0 wholly in LDS and row 2 wholly global (n_pad <=
+    // S <= 2 n_pad, the config-2 layout): only row 1's rounds choose, so
+    // four of a round's six slot accesses need no branch (a branch per access
+    // also waits for every load issued before it, breaking the load batch).
+#ifndef QKD_FIXED_ROWS
+#define QKD_FIXED_ROWS 1
+#endif
+    const bool fixed_rows = QKD_FIXED_ROWS && DV3 && n_pad <= ms.S && ms.S <= 2 * n_pad;
+    auto ld_k = [&](auto fx, int k, uint32_t iw, uint32_t i) -> double {
+        const uint32_t x = (uint32_t)k * n_pad + i;
+        if constexpr (decltype(fx)::value) {
+            if (k == 0) return ms.l[x];
+            if (k == 2) return BufIo<double>::ld(ms.g, (x - ms.S) * 8u);
+        }
+        return ms.ld_row((uint32_t)k * n_pad + iw, x);
+    };
+    auto st_k = [&](auto fx, int k, uint32_t iw, uint32_t i, double v) {
+        const uint32_t x = (uint32_t)k * n_pad + i;
+        if constexpr (decltype(fx)::value) {
+            if (k == 0) { ms.l[x] = v; return; }
+            if (k == 2) { BufIo<double>::st(ms.g, (x - ms.S) * 8u, v); return; }
+        }
+        ms.st_row((uint32_t)k * n_pad + iw, x, v);
+    };
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
     // one batch of kIvChunk rounds: its loads, then its rounds
     typedef double VB[kIvChunk][kDvUnroll];
-    auto batch_load = [&](int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
+    auto batch_load = [&](auto fx, int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
 #pragma unroll
         for (int u = 0; u < kIvChunk; ++u) {
             const int i = tid + (r0 + u) * kDecodeBlock;
-            const bool ok = i < c.n;
+            const bool ok = i < cn;
             bc[u] = ok ? c.bit_code[i] : 0;
             pat[u] = (FOLD && ftab && ok) ? (uint32_t)c.bit_pat[i] : 0u;
-            const uint32_t iw = (uint32_t)((r0 + u) * kDecodeBlock + wave * 64);
+            // (wave-uniform, said so: left to itself loop strength reduction
+            // rebuilds it from the per-lane bit index, and every row's LDS /
+            // global choice becomes a divergent branch with exec-mask shuffling)
+            const uint32_t iw = __builtin_amdgcn_readfirstlane((uint32_t)((r0 + u) * kDecodeBlock + wave * 64));
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k)
-                v[u][k] = FOLD ? 0.0 : ms.ld_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i);
+                v[u][k] = FOLD ? 0.0 : ld_k(fx, k, iw, (uint32_t)i);
         }
     };
-    auto batch_compute = [&](int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
+    auto batch_compute = [&](auto fx, int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
 #pragma unroll
         for (int u = 0; u < kIvChunk; ++u) {
             const int r = r0 + u;
-            if (r * kDecodeBlock >= c.n) break;            // block-uniform
+            if (r * kDecodeBlock >= cn) break;            // block-uniform
             const int i = tid + r * kDecodeBlock;
-            const uint32_t iw = (uint32_t)(r * kDecodeBlock + wave * 64);
+            const uint32_t iw = __builtin_amdgcn_readfirstlane((uint32_t)(r * kDecodeBlock + wave * 64));
             // a full round (block-uniform): every lane's bit exists
-            const bool full = (r + 1) * kDecodeBlock <= c.n;
-            const bool ok = full || i < c.n;
+            const bool full = (r + 1) * kDecodeBlock <= cn;
+            const bool ok = full || i < cn;
             const int deg = DV3 ? kDvUnroll : (int)(bc[u] >> 48) & 3;
             int32_t jc[kDvUnroll];
 #pragma unroll
@@ -814,7 +847,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 }
             }
             const uint64_t zb = __ballot(z);
-            if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
+            if (lane == 0 && r * kDecodeBlock + wave * 64 < cn) zw[(r * kDecodeBlock >> 6) + wave] = zb;
             if (z) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
@@ -828,8 +861,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             if (!keep) continue;
             if (DV3 && full) {
 #pragma unroll
-                for (int k = 0; k < kDvUnroll; ++k)
-                    ms.st_row((uint32_t)k * n_pad + iw, (uint32_t)k * n_pad + i, qkds::pack_iv(bo[k]));
+                for (int k = 0; k < kDvUnroll; ++k) st_k(fx, k, iw, (uint32_t)i, qkds::pack_iv(bo[k]));
             } else if (ok) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
@@ -837,33 +869,21 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             }
         }
     };
-#ifndef QKD_IV_PIPE
-#define QKD_IV_PIPE 0
-#endif
-    if constexpr (QKD_IV_PIPE && !FOLD) {
-        // software-pipelined: the next batch's loads are issued before this
-        // batch's rounds (two batches of registers)
-        VB va, vb;
-        uint64_t ba[kIvChunk], bb[kIvChunk];
-        uint32_t pa[kIvChunk], pb[kIvChunk];
-        batch_load(0, va, ba, pa);
-        for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += 2 * kIvChunk) {
-            const bool more = (r0 + kIvChunk) * kDecodeBlock < c.n;
-            if (more) batch_load(r0 + kIvChunk, vb, bb, pb);
-            batch_compute(r0, va, ba, pa);
-            if (!more) break;
-            if ((r0 + 2 * kIvChunk) * kDecodeBlock < c.n) batch_load(r0 + 2 * kIvChunk, va, ba, pa);
-            batch_compute(r0 + kIvChunk, vb, bb, pb);
-        }
-    } else {
-        for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kIvChunk) {
+    using NoFx = std::integral_constant<bool, false>;
+    using Fx = std::integral_constant<bool, true>;
+    auto run = [&](auto fx) {
+        for (int r0 = 0; __builtin_amdgcn_readfirstlane(r0 * kDecodeBlock) < cn; r0 += kIvChunk) {
             VB v;
             uint64_t bc[kIvChunk];                 // the bits' packed words (DeviceCode::bit_code)
             uint32_t pat[kIvChunk];                // FOLD with ftab: the bits' degree patterns
-            batch_load(r0, v, bc, pat);
-            batch_compute(r0, v, bc, pat);
+            batch_load(fx, r0, v, bc, pat);
+            batch_compute(fx, r0, v, bc, pat);
         }
-    }
+    };
+    if (fixed_rows)
+        run(Fx{});
+    else
+        run(NoFx{});
 }
 
 // The workgroup's global slot region. QKD_XCD_REGIONS (default): the regions
