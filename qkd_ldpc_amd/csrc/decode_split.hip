@@ -1011,15 +1011,13 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
     // atomic's round trip overlaps the prologue's loads
     if (tid == 0) ctl[1] = atomicAdd(a.counter, 1u);
     uint32_t next_f = 0;
-    // the syndrome words start each frame at zero (every round's syndrome
-    // test clears them again)
-    for (int w = tid; w < m_words; w += kDecodeBlock) {
-        xsyn[w] = 0;
-        xunc[w] = 0;
-    }
-    __syncthreads();
     for (;;) {
         pc.mark(4);
+        for (int w = tid; w < m_words; w += kDecodeBlock) {
+            xsyn[w] = 0;
+            xunc[w] = 0;
+        }
+        __syncthreads();
         const uint32_t f = ctl[1];
         if (f >= a.n_frames) break;
         if (tid == 0) next_f = atomicAdd(a.counter, 1u);
@@ -1085,11 +1083,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                 }
             }
         }
-        // (keys path with the folded first iteration: the first phase is the
-        // folded bit phase, which reads nothing init_slots wrote, and the
-        // staged Bob words are overwritten only by the first check phase,
-        // after that bit phase's barrier: no barrier here)
-        if (!(MODE == kModeKeys && fold1)) __syncthreads();
+        __syncthreads();
         pc.mark(0);
 
         // ---- iterations (:212-330): interval iterations (qkd_spec.h) in the
