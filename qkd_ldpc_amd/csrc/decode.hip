@@ -879,60 +879,74 @@ __global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_
     }
 }
 
-// The same key pair by two waves per frame (the default generator): in the
+// The same key pair by two waves per workgroup (the default generator): in the
 // one-wave form every lane's chunk mixes Alice's bits and shuffle draws, so
-// the wave runs both loop bodies on every draw. Here wave 0's 64 lanes draw
-// only Alice's bits (lane l: draws [l * cb, (l + 1) * cb), OR-ed into LDS
-// words, as chunks need not end on word boundaries) and wave 1's only the
-// shuffle's (lane l: from draw N + l * cs): each lane jumps once (its own
-// polynomial, c->d_jpoly2), every loop is uniform, and a frame has twice the
-// waves to hide its chains behind. The shuffle's low steps are replayed and
-// the last writers found exactly as in keygen_fast_kernel; the flips land in
-// an LDS copy of the key, and both keys leave as whole coalesced words.
-// LDS: low[ne], last[ne], park[ne / 2 + 1], alice[words], bob[words].
+// the wave runs both loop bodies on every draw. Here wave 0 draws only Alice's
+// bits (a frame's lane l: draws [l * cb, (l + 1) * cb), OR-ed into LDS words,
+// as chunks need not end on word boundaries) and wave 1 only the shuffle's
+// (lane l: from draw N + l * cs): each lane jumps once (its own polynomial,
+// c->d_jpoly2), every loop is uniform. A frame takes kKgSplitLanes lanes of
+// each wave, so a workgroup holds kKgSplitFrames frames: fewer lanes per
+// frame mean longer chunks but fewer 256-step jumps per frame. The shuffle's
+// low steps are replayed and the last writers found exactly as in
+// keygen_fast_kernel; the flips land in an LDS copy of the key, and both keys
+// leave as whole coalesced words.
+// LDS per frame: low[ne], last[ne], park[ne / 2 + 1], alice[words], bob[words].
 template <bool R32>
 __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
                                                            uint32_t words, uint32_t ne, uint32_t cb, uint32_t cs,
-                                                           const uint64_t* __restrict__ jpoly, uint64_t* alice_w,
-                                                           uint64_t* bob_w, double* exact_q, uint32_t force_serial) {
+                                                           uint32_t n_frames, const uint64_t* __restrict__ jpoly,
+                                                           uint64_t* alice_w, uint64_t* bob_w, double* exact_q,
+                                                           uint32_t force_serial) {
+    constexpr uint32_t KL = kKgSplitLanes, FPW = kKgSplitFrames;
     extern __shared__ uint64_t ks_lds[];
-    __shared__ uint32_t s_lone, s_reject;
-    uint32_t* low = reinterpret_cast<uint32_t*>(ks_lds);
-    uint32_t* last = low + ne;
-    uint2* park = reinterpret_cast<uint2*>(last + ne);        // 8-byte aligned: 2 ne words before it
-    uint64_t* aw = reinterpret_cast<uint64_t*>(park + ne / 2 + 1);
-    uint64_t* bw = aw + words;
-    const uint32_t f = blockIdx.x;                              // one frame per workgroup, grid = frames
+    __shared__ uint32_t s_lone[FPW], s_reject[FPW];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const bool shuffle_wave = tid >= 64;                        // wave-uniform
+    const uint32_t slot = lane / KL;                            // this lane's frame in the workgroup
+    const uint32_t l = lane % KL;                               // and its lane in that frame
+    // (per frame an even number of 32-bit words before the key words)
+    const uint32_t frame_u64 = (2 * ne + 2 * (ne / 2 + 1)) / 2 + 2 * words;
+    auto frame_lds = [&](uint32_t sl) { return ks_lds + (size_t)sl * frame_u64; };
+    uint32_t* low = reinterpret_cast<uint32_t*>(frame_lds(slot));
+    uint32_t* last = low + ne;
+    uint2* park = reinterpret_cast<uint2*>(last + ne);
+    uint64_t* aw = reinterpret_cast<uint64_t*>(park + ne / 2 + 1);
+    const uint32_t f = blockIdx.x * FPW + slot;
+    const bool live = f < n_frames;                             // (the last workgroup may hold fewer)
     const bool even = (n & 1u) == 0;
     const uint64_t pair0 = even ? (uint64_t)n + 1 : (uint64_t)n;
     const uint32_t i0 = even ? 2u : 1u;
     const uint64_t draws = qkdr::trial_draws(n);
 
     qkdr::Xoshiro256pp g;
-    g.seed(seeds[f] + offset);
+    g.seed(live ? seeds[f] + offset : 0);
     {
         uint64_t st[4] = {g.s0, g.s1, g.s2, g.s3};
-        const uint64_t p[4] = {jpoly[tid * 4 + 0], jpoly[tid * 4 + 1], jpoly[tid * 4 + 2], jpoly[tid * 4 + 3]};
+        const uint32_t pi = (shuffle_wave ? KL : 0u) + l;
+        const uint64_t p[4] = {jpoly[pi * 4 + 0], jpoly[pi * 4 + 1], jpoly[pi * 4 + 2], jpoly[pi * 4 + 3]};
         qkdr::jump_poly_apply(p, st);
         g.s0 = st[0]; g.s1 = st[1]; g.s2 = st[2]; g.s3 = st[3];
     }
-    for (uint32_t q = tid; q < ne; q += 128) {
-        low[q] = q;
-        last[q] = 0;
+    for (uint32_t sl = 0; sl < FPW; ++sl) {
+        uint32_t* lo = reinterpret_cast<uint32_t*>(frame_lds(sl));
+        uint64_t* a = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(lo + 2 * ne) + ne / 2 + 1);
+        for (uint32_t q = tid; q < ne; q += 128) {
+            lo[q] = q;
+            lo[ne + q] = 0;
+        }
+        for (uint32_t w = tid; w < words; w += 128) a[w] = 0;
     }
-    for (uint32_t w = tid; w < words; w += 128) aw[w] = 0;
-    if (tid == 0) {
-        s_lone = 0;
-        s_reject = force_serial;
+    if (tid < FPW) {
+        s_lone[tid] = 0;
+        s_reject[tid] = force_serial;
     }
     __syncthreads();
 
     if (!shuffle_wave) {
-        const uint32_t first = lane * cb;
-        const uint32_t end = min(first + cb, n);
+        const uint32_t first = l * cb;
+        const uint32_t end = live ? min(first + cb, n) : first;
         uint64_t acc = 0;
         for (uint32_t d = first; d < end; ++d) {
             acc |= (g.next() >> 63) << (d & 63u);
@@ -942,12 +956,12 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
             }
         }
     } else {
-        const uint64_t first = (uint64_t)n + (uint64_t)lane * cs;
-        const uint64_t end = min(first + cs, draws);
+        const uint64_t first = (uint64_t)n + (uint64_t)l * cs;
+        const uint64_t end = live ? min(first + cs, draws) : first;
         for (uint64_t d = first; d < end; ++d) {
             const uint64_t r = g.next();
             if (d < pair0) {
-                s_lone = (uint32_t)(r >> 63);
+                s_lone[slot] = (uint32_t)(r >> 63);
                 continue;
             }
             const uint32_t i = i0 + 2u * (uint32_t)(d - pair0);
@@ -961,7 +975,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
                 const uint64_t p1 = (uint64_t)(uint32_t)(r >> 32) * rg;
                 const uint64_t lo = p0 + (p1 << 32);
                 if (lo < range) {
-                    if (lo < (0 - range) % range) s_reject = 1;
+                    if (lo < (0 - range) % range) s_reject[slot] = 1;
                 }
                 const uint32_t x = (uint32_t)((p1 + (p0 >> 32)) >> 32);
                 uint32_t q = (uint32_t)((float)x * __builtin_amdgcn_rcpf((float)bb));
@@ -972,7 +986,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
                 qb = (uint32_t)rem;
             } else {
                 const uint64_t lo = r * range;
-                if (lo < range && lo < (0 - range) % range) s_reject = 1;
+                if (lo < range && lo < (0 - range) % range) s_reject[slot] = 1;
                 const uint64_t x = qkdr::mul_hi64(r, range);
                 uint64_t a = (uint64_t)((double)x / (double)b1);
                 if (a * b1 > x) --a;
@@ -992,25 +1006,23 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
 
     uint64_t* A = alice_w + (size_t)f * words;
     uint64_t* B = bob_w + (size_t)f * words;
-    if (s_reject) {
+    const bool rej = live && s_reject[slot];
+    if (rej && !shuffle_wave && l == 0) {
         // exact serial regeneration of this frame (never observed in practice)
-        if (tid == 0) {
-            qkdr::Xoshiro256pp h;
-            h.seed(seeds[f] + offset);
-            for (uint32_t w = 0; w < words; ++w) {
-                const uint32_t nb = min(64u, n - w * 64);
-                uint64_t v = 0;
-                for (uint32_t b = 0; b < nb; ++b) v |= (h.next() >> 63) << b;
-                A[w] = v;
-                B[w] = v;
-            }
-            qkdr::shuffle_low_positions(h, n, ne, low);
-            for (uint32_t q = 0; q < ne; ++q) B[low[q] >> 6] ^= 1ull << (low[q] & 63);
-            if (exact_q) exact_q[f] = (double)ne / (double)n;
+        qkdr::Xoshiro256pp h;
+        h.seed(seeds[f] + offset);
+        for (uint32_t w = 0; w < words; ++w) {
+            const uint32_t nb = min(64u, n - w * 64);
+            uint64_t v = 0;
+            for (uint32_t b = 0; b < nb; ++b) v |= (h.next() >> 63) << b;
+            A[w] = v;
+            B[w] = v;
         }
-        return;                                                // (workgroup-uniform)
+        qkdr::shuffle_low_positions(h, n, ne, low);
+        for (uint32_t q = 0; q < ne; ++q) B[low[q] >> 6] ^= 1ull << (low[q] & 63);
+        if (exact_q) exact_q[f] = (double)ne / (double)n;
     }
-    if (tid == 64) {
+    if (live && !rej && shuffle_wave && l == 0) {
         // replay of the steps with index < ne (shuffle_low_positions' step())
         auto step = [&](uint32_t si, uint32_t x) {
             if (si < ne) {
@@ -1022,7 +1034,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
             }
         };
         if (n > 1) {
-            if (even) step(1, s_lone);
+            if (even) step(1, s_lone[slot]);
             for (uint32_t i = i0; i < ne && i < n; i += 2) {
                 const uint2 q = park[(i - i0) >> 1];
                 step(i, q.x);
@@ -1031,16 +1043,33 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         }
         if (exact_q) exact_q[f] = (double)ne / (double)n;
     }
-    for (uint32_t w = tid; w < words; w += 128) bw[w] = aw[w];
-    __syncthreads();
-    for (uint32_t q = tid; q < ne; q += 128) {
-        const uint32_t pos = last[q] ? last[q] : low[q];
-        atomicXor(reinterpret_cast<unsigned long long*>(&bw[pos >> 6]), 1ull << (pos & 63u));
+    // (the rest per frame slot, all 128 threads; a rejected frame is done)
+    for (uint32_t sl = 0; sl < FPW; ++sl) {
+        uint64_t* a = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(
+                          reinterpret_cast<uint32_t*>(frame_lds(sl)) + 2 * ne) + ne / 2 + 1);
+        for (uint32_t w = tid; w < words; w += 128) a[words + w] = a[w];
     }
     __syncthreads();
-    for (uint32_t w = tid; w < words; w += 128) {
-        A[w] = aw[w];
-        B[w] = bw[w];
+    for (uint32_t sl = 0; sl < FPW; ++sl) {
+        const uint32_t fs = blockIdx.x * FPW + sl;
+        if (fs >= n_frames || s_reject[sl]) continue;                // (workgroup-uniform)
+        uint32_t* lo = reinterpret_cast<uint32_t*>(frame_lds(sl));
+        uint64_t* b = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(lo + 2 * ne) + ne / 2 + 1) + words;
+        for (uint32_t q = tid; q < ne; q += 128) {
+            const uint32_t pos = lo[ne + q] ? lo[ne + q] : lo[q];
+            atomicXor(reinterpret_cast<unsigned long long*>(&b[pos >> 6]), 1ull << (pos & 63u));
+        }
+    }
+    __syncthreads();
+    for (uint32_t sl = 0; sl < FPW; ++sl) {
+        const uint32_t fs = blockIdx.x * FPW + sl;
+        if (fs >= n_frames || s_reject[sl]) continue;
+        const uint64_t* a = reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint2*>(
+                                reinterpret_cast<const uint32_t*>(frame_lds(sl)) + 2 * ne) + ne / 2 + 1);
+        for (uint32_t w = tid; w < words; w += 128) {
+            alice_w[(size_t)fs * words + w] = a[w];
+            bob_w[(size_t)fs * words + w] = a[words + w];
+        }
     }
 }
 
@@ -1823,12 +1852,13 @@ static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uin
     const bool matrix = mode && !strcmp(mode, "matrix");
     const bool lanes = mode && !strcmp(mode, "lanes");
     // the two-wave generator (default; QKD_KEYGEN=replay forces its serial path)
-    const size_t lds2 = (2 * (size_t)ne + 2 * (ne / 2 + 1)) * sizeof(uint32_t) + 2 * (size_t)words * sizeof(uint64_t);
+    const size_t lds2 = (size_t)kKgSplitFrames * ((2 * (size_t)ne + 2 * (ne / 2 + 1)) * sizeof(uint32_t) +
+                                                  2 * (size_t)words * sizeof(uint64_t));
     if (ne <= kKeygenFastMaxErrors && c->d_jpoly2 && !serial && !matrix && !lanes && lds2 <= kLdsBytesMax) {
         auto* const kg = c->n <= 65536 ? keygen_split_kernel<true> : keygen_split_kernel<false>;
-        hipLaunchKernelGGL(kg, dim3((unsigned)n_frames), dim3(128), lds2, stream, seeds, offset, (uint32_t)c->n,
-                           words, (uint32_t)ne, c->kg_cb, c->kg_cs, c->d_jpoly2, ws->alice_w, ws->bob_w, exact_q,
-                           replay);
+        hipLaunchKernelGGL(kg, dim3((unsigned)((n_frames + kKgSplitFrames - 1) / kKgSplitFrames)), dim3(128), lds2,
+                           stream, seeds, offset, (uint32_t)c->n, words, (uint32_t)ne, c->kg_cb, c->kg_cs,
+                           (uint32_t)n_frames, c->d_jpoly2, ws->alice_w, ws->bob_w, exact_q, replay);
         QKD_HIP(hipGetLastError());
         return QKD_OK;
     }

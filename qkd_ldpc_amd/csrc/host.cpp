@@ -247,18 +247,20 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         return set_error(QKD_ERR_DEVICE, "xoshiro256 characteristic polynomial: unexpected degree");
     QKD_HIP(hipMalloc(&c->d_jpoly, jp.size() * sizeof(uint64_t)));
     QKD_HIP(hipMemcpy(c->d_jpoly, jp.data(), jp.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-    // the two-wave generator's starts (keygen_split_kernel): Alice's bits in 64
-    // chunks of kg_cb, the shuffle draws (from draw N) in 64 chunks of kg_cs
+    // the two-wave generator's starts (keygen_split_kernel): Alice's bits in
+    // kKgSplitLanes chunks of kg_cb, the shuffle draws (from draw N) in
+    // kKgSplitLanes chunks of kg_cs
     {
         uint64_t P[4];
         if (!qkdr::xoshiro_charpoly(P))
             return set_error(QKD_ERR_DEVICE, "xoshiro256 characteristic polynomial: unexpected degree");
-        c->kg_cb = (uint32_t)((n + 63) / 64);
-        c->kg_cs = (uint32_t)((draws - (uint64_t)n + 63) / 64);
-        std::vector<uint64_t> jp2(128 * 4);
-        for (int l = 0; l < 64; ++l) {
+        const uint32_t kl = kKgSplitLanes;
+        c->kg_cb = (uint32_t)((n + kl - 1) / kl);
+        c->kg_cs = (uint32_t)((draws - (uint64_t)n + kl - 1) / kl);
+        std::vector<uint64_t> jp2((size_t)2 * kl * 4);
+        for (uint32_t l = 0; l < kl; ++l) {
             qkdr::poly_x_pow((uint64_t)l * c->kg_cb, P, &jp2[(size_t)l * 4]);
-            qkdr::poly_x_pow((uint64_t)n + (uint64_t)l * c->kg_cs, P, &jp2[(size_t)(64 + l) * 4]);
+            qkdr::poly_x_pow((uint64_t)n + (uint64_t)l * c->kg_cs, P, &jp2[(size_t)(kl + l) * 4]);
         }
         QKD_HIP(hipMalloc(&c->d_jpoly2, jp2.size() * sizeof(uint64_t)));
         QKD_HIP(hipMemcpy(c->d_jpoly2, jp2.data(), jp2.size() * sizeof(uint64_t), hipMemcpyHostToDevice));

@@ -46,6 +46,14 @@ constexpr int kKeygenLanes = 1 << kKeygenLevels;
 constexpr int kKeygenBlock = kKeygenLanes < 64 ? 64 : kKeygenLanes;   // threads per workgroup
 constexpr int kKeygenFrames = kKeygenBlock / kKeygenLanes;
 constexpr uint32_t kKeygenFastMaxErrors = 4096;
+// keygen_split_kernel: lanes per frame in each of its two waves (Alice's bits,
+// shuffle draws), so 64 / kKgSplitLanes frames per 128-thread workgroup
+#ifndef QKD_KG_SPLIT_LANES
+#define QKD_KG_SPLIT_LANES 64
+#endif
+constexpr uint32_t kKgSplitLanes = QKD_KG_SPLIT_LANES;
+constexpr uint32_t kKgSplitFrames = 64 / kKgSplitLanes;
+static_assert(kKgSplitLanes >= 1 && 64 % kKgSplitLanes == 0, "lanes per frame divide a wave");
 
 // Device-resident, immutable view of H.
 //   chk_bits[k * m_pad + j]  bit index of slot k of check j (ascending), -1 pad
@@ -166,9 +174,10 @@ struct qkd_code {
     uint64_t* d_jump = nullptr;
     // the same jumps as polynomials: d_jpoly[l] = x^(l * chunk) mod P (4 words)
     uint64_t* d_jpoly = nullptr;
-    // keygen_split_kernel (the default): wave 0's lane l draws Alice's bits
-    // [l * kg_cb, (l + 1) * kg_cb), wave 1's lane l the shuffle draws from
-    // N + l * kg_cs; d_jpoly2[w * 64 + l] = x^(start) mod P
+    // keygen_split_kernel (the default): a frame's lane l of wave 0 draws
+    // Alice's bits [l * kg_cb, (l + 1) * kg_cb), its lane l of wave 1 the
+    // shuffle draws from N + l * kg_cs; d_jpoly2[w * kKgSplitLanes + l] =
+    // x^(start) mod P
     uint32_t kg_cb = 0, kg_cs = 0;
     uint64_t* d_jpoly2 = nullptr;
     int cu_count = 0;
