@@ -329,13 +329,35 @@ inline bool xoshiro_jump_polys(uint64_t chunk, int lanes, uint64_t* out) {
 QKD_RHD void jump_poly_apply(const uint64_t p[4], uint64_t s[4]) {
     uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     uint64_t t[4] = {s[0], s[1], s[2], s[3]};
-    for (int w = 0; w < 4; ++w) {
-        const uint64_t pw = p[w];
 #if defined(__HIP_DEVICE_COMPILE__)
+    // gfx950: a coefficient's mask is one sign-extended bit field extract
+    // (v_bfe_i32), and each 32-bit half of a ^= t & m one v_bitop3_b32 (truth
+    // table f(a, t, m) = a ^ (t & m) = 0xF0 ^ (0xCC & 0xAA) = 0x78)
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int w = 0; w < 8; ++w) {
+        const int pw = (int)(uint32_t)(p[w >> 1] >> (32 * (w & 1)));
 #pragma unroll 8
-#endif
-        for (int j = 0; j < 64; ++j) {
-            const uint64_t m = (uint64_t)0 - ((pw >> j) & 1u);
+        for (int j = 0; j < 32; ++j) {
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe(pw, j, 1);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                h[2 * k] = __builtin_amdgcn_bitop3_b32(h[2 * k], (uint32_t)t[k], m, (unsigned char)0x78);
+                h[2 * k + 1] = __builtin_amdgcn_bitop3_b32(h[2 * k + 1], (uint32_t)(t[k] >> 32), m, (unsigned char)0x78);
+            }
+            xoshiro_step_state(t);
+        }
+    }
+    a0 = ((uint64_t)h[1] << 32) | h[0];
+    a1 = ((uint64_t)h[3] << 32) | h[2];
+    a2 = ((uint64_t)h[5] << 32) | h[4];
+    a3 = ((uint64_t)h[7] << 32) | h[6];
+#else
+    // over 32-bit halves of p (the device form's order)
+    for (int w = 0; w < 8; ++w) {
+        const uint32_t pw = (uint32_t)(p[w >> 1] >> (32 * (w & 1)));
+        for (int j = 0; j < 32; ++j) {
+            const uint32_t m32 = 0u - ((pw >> j) & 1u);
+            const uint64_t m = ((uint64_t)m32 << 32) | m32;
             a0 ^= t[0] & m;
             a1 ^= t[1] & m;
             a2 ^= t[2] & m;
@@ -343,6 +365,7 @@ QKD_RHD void jump_poly_apply(const uint64_t p[4], uint64_t s[4]) {
             xoshiro_step_state(t);
         }
     }
+#endif
     s[0] = a0;
     s[1] = a1;
     s[2] = a2;
