@@ -74,8 +74,14 @@ def parse():
     ap.add_argument("--kernel-events", choices=["on", "off"], default="on",
                     help="HIP events around each decoder launch inside the timed loop (off: diagnostics)")
     ap.add_argument("--no-sweeps", action="store_true",
-                    help="skip the config-3 QBER sweep and the config-4 rank-share lines")
-    return ap.parse_args()
+                    help="skip the config-3 QBER sweep (and config 4, as --config4-frames 0)")
+    ap.add_argument("--config4-frames", type=int, default=None,
+                    help="frames of the configs[3] run sharded over the ranks (default 1,000,000, "
+                         "0 with --no-sweeps; 0 disables)")
+    args = ap.parse_args()
+    if args.config4_frames is None:
+        args.config4_frames = 0 if args.no_sweeps else 1_000_000
+    return args
 
 
 def load_code(device):
@@ -115,41 +121,91 @@ def rocprof_warm_ms(kernel):
     return None, None
 
 
+N_SIMD = 1024            # 256 CUs x 4 SIMD-32 units
+VALU_ISSUE_CYC = 2.0     # cycles per wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md)
+RATED_CLOCK_GHZ = 2.4    # MI355X peak engine clock
+
+
+def issue_ceiling_4waves():
+    """Cycles per wave-instruction per SIMD that 4 waves per SIMD (this decoder's
+    occupancy: one 1024-thread workgroup per CU) sustain at ILP 8, by instruction kind,
+    from the newest committed tools/mb/issue_mb.hip record (profiles/r*_issue_mb.txt)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_issue_mb.txt")))
+    if not files:
+        return None
+    out = {}
+    with open(files[-1]) as f:
+        for line in f:
+            p = line.split()
+            # "<inst> waves/SIMD <w> ILP <k> cycles/wave-inst/SIMD <c>"
+            if len(p) == 7 and p[1] == "waves/SIMD" and float(p[2]) == 4.0 and p[4] == "8":
+                out[p[0]] = float(p[6])
+    return {"cycles_per_wave_inst": out, "source": os.path.relpath(files[-1], ROOT)} if out else None
+
+
 def roofline_block(variant, alg_bytes, kernel_s, call_s, kernel_name):
-    """roofline (the contract's block): algorithmic bytes per launch
-    / the DECODE KERNEL's average duration, measured live with HIP events recorded
-    around its launch on its own stream (qkd_debug_decoder_timing), against the 8 TB/s
-    HBM peak. `frac` is nominal: this formulation moves far fewer bytes than the
-    reference's two-array one. Alongside:
-      frac_call     the same bytes over the whole library call (pack, frame syndromes,
-                    decoder, key compare: HIP events around the call);
-      frac_kernel   the same bytes over the committed rocprof warm average of the kernel;
-      binding       what the PMC record of the kernel measured: DRAM bytes per launch
-                    as a fraction of the HBM peak over this kernel time, and the VALU
-                    active fraction (SQ_ACTIVE_INST_VALU x 4 quad-cycles / cycles x SIMDs);
-                    `limiter` names the larger."""
-    achieved = alg_bytes / kernel_s / 1e9
+    """roofline (the contract's block) for the decode kernel, bound by what binds it.
+
+    The decoder is VALU-issue / latency bound, not HBM bound: its
+    speculative rounds run binary32 intervals and most message slots sit in LDS, so it
+    never moves the reference's two-array binary64 bytes. The headline is therefore
+    the VALU issue fraction from the kernel's PMC record (separate rocprofv3 --pmc
+    passes, tools/pmc_traffic.py), reproducible from that file alone:
+        frac = SQ_INSTS_VALU x 2 cycles / (kernel cycles x 1024 SIMDs)
+    with kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs of the counted dispatches;
+    achieved = SQ_INSTS_VALU / (the counted dispatches' own duration) and peak =
+    1024 SIMDs / 2 cycles x their effective clock, so frac = achieved / peak.
+    Beside it:
+      live              the same instruction count over THIS run's decoder time (HIP
+                        events around each launch on its stream), at the PMC pass's
+                        effective clock and at the rated 2.4 GHz;
+      hbm_frac_measured the PMC record's HBM bytes (FETCH_SIZE x2 + WRITE_SIZE) per
+                        launch over the counted dispatches' duration, / 8 TB/s;
+      nominal_frac      SURVEY.md §8(d)'s algorithmic bytes (the reference's two-array
+                        binary64 traffic at the executed iterations) over the live kernel
+                        time / 8 TB/s -- above 1 when the kernel finishes sooner than any
+                        HBM-bound implementation of that formulation could: it is NOT an
+                        achieved bandwidth;
+      issue_ceiling_4waves  what 4 waves per SIMD sustain per instruction kind
+                        (tools/mb/issue_mb.hip), a second reference point."""
     rec, src = pmc_record(variant)
-    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": achieved / HBM_PEAK_GBS, "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
-           "nominal": True, "kernel": kernel_name, "kernel_ms": kernel_s * 1e3, "call_ms": call_s * 1e3,
-           "frac_call": alg_bytes / call_s / 1e9 / HBM_PEAK_GBS,
-           "algorithmic_bytes_per_launch": alg_bytes, "traffic_source": src}
-    if rec:
-        out["pmc_kernel"] = rec.get("kernel")
-        warm, wsrc = rocprof_warm_ms(rec.get("kernel"))
-        if warm:
-            out["frac_kernel"] = alg_bytes / (warm / 1e3) / 1e9 / HBM_PEAK_GBS
-            out["rocprof_warm_ms"] = warm
-            out["rocprof_source"] = wsrc
-        v = rec.get("valu", {})
-        dram = rec["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS
-        act = v.get("valu_active_util_x4")
-        out["binding"] = {"dram_frac": dram, "valu_active_frac": act,
-                          "valu_insts_per_launch": v.get("valu_insts_per_launch"),
-                          "wait_frac": v.get("wait_frac"), "lds_conflict_frac": v.get("lds_conflict_frac"),
-                          "effective_clock_ghz": v.get("effective_clock_ghz"),
-                          "limiter": "valu" if (act or 0) > dram else "hbm"}
+    nominal = alg_bytes / kernel_s / 1e9 / HBM_PEAK_GBS
+    base = {"kernel": kernel_name, "kernel_ms": kernel_s * 1e3, "call_ms": call_s * 1e3,
+            "algorithmic_bytes_per_launch": alg_bytes, "nominal_frac": nominal,
+            "nominal_note": "SURVEY.md §8(d) bytes / live kernel time / 8 TB/s; exceeds 1 because this kernel "
+                            "does not move the reference's two-array fp64 bytes -- not an achieved bandwidth",
+            "nominal_frac_call": alg_bytes / call_s / 1e9 / HBM_PEAK_GBS}
+    v = (rec or {}).get("valu", {})
+    insts, cyc, clk = v.get("valu_insts_per_launch"), v.get("gpu_cycles"), v.get("effective_clock_ghz")
+    if not (rec and insts and cyc and clk):
+        # no PMC record: only the nominal HBM figure is available (marked so)
+        return {"bound": "hbm", "achieved": alg_bytes / kernel_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": nominal, "traffic": None, "nominal": True, **base}
+    pmc_s = cyc / (clk * 1e9)                        # the counted dispatches' duration
+    frac = insts * VALU_ISSUE_CYC / (cyc * N_SIMD)
+    peak = N_SIMD / VALU_ISSUE_CYC * clk             # G wave-instructions / s
+    out = {"bound": "valu", "achieved": insts / pmc_s / 1e9, "peak": peak, "unit": "G wave-inst/s",
+           "frac": frac, "traffic": rec.get("hbm_bytes_per_launch"),
+           "formula": "frac = SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE/8 x 1024) of the PMC record",
+           "pmc_source": src, "pmc_kernel": rec.get("kernel"),
+           "valu_insts_per_launch": insts, "pmc_kernel_cycles": cyc, "pmc_clock_ghz": clk,
+           "pmc_kernel_ms": pmc_s * 1e3,
+           "hbm_frac_measured": rec["hbm_bytes_per_launch"] / pmc_s / 1e9 / HBM_PEAK_GBS,
+           "live": {"kernel_ms": kernel_s * 1e3,
+                    "frac_at_pmc_clock": insts * VALU_ISSUE_CYC / (kernel_s * clk * 1e9 * N_SIMD),
+                    "frac_at_rated_clock": insts * VALU_ISSUE_CYC / (kernel_s * RATED_CLOCK_GHZ * 1e9 * N_SIMD)},
+           "valu_active_frac": v.get("valu_active_util_x4"), "wait_frac": v.get("wait_frac"),
+           "lds_conflict_frac": v.get("lds_conflict_frac"), **base}
+    ceil = issue_ceiling_4waves()
+    if ceil:
+        c = ceil["cycles_per_wave_inst"]
+        out["issue_ceiling_4waves"] = ceil
+        if "v_fma_f32" in c:
+            out["frac_of_4wave_fma_ceiling"] = insts * c["v_fma_f32"] / (cyc * N_SIMD)
+    warm, wsrc = rocprof_warm_ms(rec.get("kernel"))
+    if warm:
+        out["rocprof_warm_ms"] = warm
+        out["rocprof_source"] = wsrc
     return out
 
 
@@ -191,9 +247,6 @@ def measure_variants(args, step, stream, counters, iters, Q, F, q, L, ws, steps=
         b_iter = B_ITER if v == "sp_f64" else B_ITER32
         alg = int(iters.cpu().numpy().astype(np.int64).sum()) * b_iter + F * B_FRAME
         rb = roofline_block(v, alg, kms / 1e3, cms / 1e3, f"decoder kernel of qkd_qkd_ldpc_batch, variant {v}")
-        if "binding" in rb:
-            rb["bound"] = rb["binding"]["limiter"]
-            rb["nominal_hbm_frac"] = rb["frac"]
         out[v] = {"value": F * N_BITS * steps / el, "unit": "bit/s", "kernel_ms": kms, "call_ms": cms,
                   "fer": st["fer"], "mean_iterations": st["iterations_successful_sp_mean"], "roofline": rb}
     return out
@@ -259,27 +312,64 @@ def config3_sweep(args, H, Q, dev):
             "reference_total_s_8_xeon_threads": 145.5, "points": points}
 
 
-def config4_rank_share(args, H, Q, dev, frames=125_000):
-    """BASELINE configs[3] on one GPU: one rank's share of the 1M-frame config-2 run over
-    8 GPUs, 125,000 frames (seeds[0:125000]) in ONE qkd_trials_batch (device keygen
-    included), timed warm."""
+def config4_fixture_counters(frames):
+    """The qkd_counters record (include/qkd_ldpc.h) of config-4 frames [0, frames)
+    from the oracle's per-frame fixture tests/golden/config4_1m.npz, or None when the
+    run is longer than the fixture."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "config4_1m.npz"))
+    n = z["iters"].size
+    if frames > n:
+        return None
+    sp = np.unpackbits(z["sp"])[:frames].astype(bool)
+    ko = np.unpackbits(z["ko"])[:frames].astype(bool)
+    it = z["iters"][:frames][sp].astype(np.uint64)
+    return {"frames": frames, "sp_ok": int(sp.sum()), "ldpc_ok": int((sp & ko).sum()),
+            "sum_iters": int(it.sum()), "sum_iters_sq": int((it * it).sum()),
+            "min_iters": int(it.min()) if it.size else 0xFFFFFFFF, "max_iters": int(it.max()) if it.size else 0}
+
+
+def config4(args, H, Q, dev, rank, world):
+    """BASELINE configs[3]: the config-2 point with --config4-frames (1,000,000) frames
+    sharded over the ranks (the reference's thread-pool fan-out
+    simulation.cpp:230-250 and its reduction :252-312). Rank r takes
+    shard_range(r, world, F) of the one seed stream, runs ONE qkd_trials_batch (device
+    keygen + frame syndromes + decode + key compare + counters), and the counters are
+    all-reduced (RCCL under torchrun / --gpus N). Timed between a barrier +
+    synchronize on both sides, max over ranks; an untimed run of the same shard first
+    (workspace allocation, clocks). value = F * N bits / that time."""
     import torch
-    seeds = torch.from_numpy(Q.make_seeds(args.seed, frames).view(np.int64)).to(dev)
+    from qkd_ldpc_amd.dist import run_sharded_point
+    F = args.config4_frames
     ws = Q.Workspace(H)
-    r = Q.run_trials(H, seeds, args.qber, 0, args.max_iters, args.threshold, True, workspace=ws)
-    torch.cuda.synchronize()
-    reps = 3
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        Q.run_trials(H, seeds, args.qber, 0, args.max_iters, args.threshold, True, workspace=ws, out=r)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
-    st = Q.counters_to_stats(Q.read_counters(r.counters), frames, args.max_iters, float(r.exact_qber[0].item()))
+    res = {}
+
+    def run_shard(b, e):
+        if "r" not in res:
+            res["seeds"] = torch.from_numpy(Q.make_seeds(args.seed, e)[b:e].view(np.int64)).to(dev)
+            res["r"] = Q.run_trials(H, res["seeds"], args.qber, 0, args.max_iters, args.threshold, True,
+                                    workspace=ws)
+        else:
+            Q.run_trials(H, res["seeds"], args.qber, 0, args.max_iters, args.threshold, True, workspace=ws,
+                         out=res["r"])
+        return res["r"].counters
+
+    counters, dt, (b, e) = run_sharded_point(rank, world, F, run_shard, torch.cuda.synchronize)
+    c = Q.read_counters(counters)
+    q = float(res["r"].exact_qber[0].item())
     ws.close()
-    return {"what": "configs[3] rank share: 125,000 config-2 frames in one qkd_trials_batch (keygen + decode + "
-                    "counters), warm, mean of 3", "frames": frames, "ms": dt * 1e3,
-            "value": frames * N_BITS / dt, "unit": "bit/s", "fer": st["fer"],
-            "sum_iterations": st["sum_iters_sp"], "mean_iterations": st["iterations_successful_sp_mean"]}
+    got = {"frames": int(c.frames), "sp_ok": int(c.sp_ok), "ldpc_ok": int(c.ldpc_ok),
+           "sum_iters": int(c.sum_iters), "sum_iters_sq": int(c.sum_iters_sq),
+           "min_iters": int(c.min_iters), "max_iters": int(c.max_iters)}
+    want = config4_fixture_counters(F)
+    st = Q.counters_to_stats(c, F, args.max_iters, q)
+    return {"what": f"configs[3]: {F} config-2 frames over {world} rank(s), one qkd_trials_batch per rank "
+                    "(keygen + decode + counters), counters all-reduced, max-rank time",
+            "frames": F, "n_gpus": world, "frames_per_rank": e - b, "ms": dt * 1e3,
+            "value": F * N_BITS / dt, "unit": "bit/s", "fer": st["fer"],
+            "sum_iterations": got["sum_iters"], "mean_iterations": st["iterations_successful_sp_mean"],
+            "std_iterations": st["iterations_successful_sp_std_dev"], "counters": got,
+            "matches_fixture": (got == want) if want is not None else None,
+            "fixture": "tests/golden/config4_1m.npz (oracle per-frame results, frames [0, F))"}
 
 
 def cpu_calibration():
@@ -511,7 +601,11 @@ def main():
             out["variants"] = measure_variants(args, step, stream, counters, iters, Q, F, q, L, ws)
         if world == 1 and not args.no_sweeps:
             out["config3_sweep"] = config3_sweep(args, H, Q, dev)
-            out["config4_rank_share"] = config4_rank_share(args, H, Q, dev)
+    # BASELINE configs[3] on every rank (a collective: all ranks take part)
+    c4 = config4(args, H, Q, dev, rank, world) if args.config4_frames > 0 else None
+    if rank == 0:
+        if c4 is not None:
+            out["config4"] = c4
         if world == 1 and not args.no_cpu_baseline and args.cpu_frames > 0:
             out["cpu_baseline"] = cpu_baseline(args, g)
         print(json.dumps(out), flush=True)

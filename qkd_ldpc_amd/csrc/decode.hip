@@ -1253,6 +1253,10 @@ static size_t decode_lds_bytes(const qkd_code* c, int dc, int tab2_entries, int 
 }
 
 static constexpr size_t kLdsBytesMax = 160 * 1024;
+// the split decoders' encoded slot words (qkd_decode.h encode_slot): a global
+// slot's word, kSlotGlobalBase + offset, must be an LDS address past any
+// allocation (its LDS access then reads 0 and drops the store)
+static_assert(kLdsBytesMax <= kSlotGlobalBase, "global slot words must lie past the LDS");
 
 static int dc_bucket(int max_dc) {
     return max_dc <= 4 ? 4 : max_dc <= 6 ? 6 : max_dc <= 8 ? 8 : max_dc <= 16 ? 16 : 64;
@@ -1378,16 +1382,49 @@ struct WsSession {
 static unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 // qkd_debug_decoder_timing: one event recorded on the launch stream before
-// and one after each decoder kernel while timing is on (events pooled per ws)
+// and one after each decoder kernel while timing is on (events pooled per ws;
+// at kDecEvPairsMax recorded pairs the finished ones are folded into a running
+// total, so the pool stays bounded)
+static constexpr size_t kDecEvPairsMax = 256;
+static hipError_t decoder_events_fold(qkd_workspace* ws) {
+    const size_t pairs = ws->dec_ev_used / 2;
+    for (size_t k = 0; k < pairs; ++k) {
+        hipError_t r = hipEventSynchronize(ws->dec_ev[2 * k + 1]);
+        float ms = 0.0f;
+        if (r == hipSuccess) r = hipEventElapsedTime(&ms, ws->dec_ev[2 * k], ws->dec_ev[2 * k + 1]);
+        if (r != hipSuccess) return r;
+        ws->dec_ms_folded += ms;
+    }
+    ws->dec_pairs_folded += pairs;
+    ws->dec_ev_used = 0;
+    return hipSuccess;
+}
+// the start event of a launch (stop: decoder_event_close)
 static hipError_t decoder_event(qkd_workspace* ws, hipStream_t stream) {
     if (!ws->time_decoder) return hipSuccess;
-    if (ws->dec_ev_used == ws->dec_ev.size()) {
+    if (ws->dec_ev_used >= 2 * kDecEvPairsMax) {
+        const hipError_t r = decoder_events_fold(ws);
+        if (r != hipSuccess) return r;
+    }
+    while (ws->dec_ev.size() < ws->dec_ev_used + 2) {
         hipEvent_t e = nullptr;
         const hipError_t r = hipEventCreate(&e);
         if (r != hipSuccess) return r;
         ws->dec_ev.push_back(e);
     }
-    return hipEventRecord(ws->dec_ev[ws->dec_ev_used++], stream);
+    const hipError_t r = hipEventRecord(ws->dec_ev[ws->dec_ev_used], stream);
+    if (r == hipSuccess) ws->dec_ev_used++;
+    return r;
+}
+// after the launch: its stop event, or, when the launch (`launch`) or the
+// record failed, the start event taken back, so pairs stay (start, stop)
+static hipError_t decoder_event_close(qkd_workspace* ws, hipStream_t stream, hipError_t launch) {
+    if (!ws->time_decoder) return launch;
+    hipError_t r = launch;
+    if (r == hipSuccess) r = hipEventRecord(ws->dec_ev[ws->dec_ev_used], stream);
+    if (r == hipSuccess) ws->dec_ev_used++;
+    else ws->dec_ev_used--;
+    return r;
 }
 
 // DeviceCode::plan_slot encoded for a split-kernel layout and check-degree
@@ -1511,11 +1548,13 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             if (const char* e = getenv("QKD_C2B_PAD")) pad = (size_t)atol(e);
             pad = std::min(pad, (size_t)c->n_pad);   // the region stays inside ws_reserve_decode's
             a.c2b_stride = ((slots - L.S + 31) & ~(size_t)31) + pad;
+            // an encoded global slot word (kSlotGlobalBase + byte offset) must
+            // stay below kSlotLds, the LDS words' tag bit
+            if (rule == kRuleSp64 && kSlotGlobalBase + a.c2b_stride * sizeof(double) >= kSlotLds)
+                return set_error(QKD_ERR_UNSUPPORTED, "code too large for the split decoder's slot words "
+                                                      "(%zu global slots per frame)", a.c2b_stride);
             a.lds_budget = (uint32_t)budget;
             a.counter = ws->counter;
-            // [0] frame queue, [1] replays: zeroed by frame_syn_kernel on the
-            // keys path (it runs first on this stream), by a memset otherwise
-            if (mode != kModeKeys) QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));
             static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;
             a.phase = nullptr;
             if (timing) {
@@ -1524,10 +1563,16 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             }
             a.replay_count = ws->counter + 1;
             a.spec_replays = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 120);
+            // [0] frame queue, [1] replays: zeroed by frame_syn_kernel on the
+            // keys path (it runs first on this stream: block 0 writes both
+            // words), by a memset otherwise -- one branch, so a keys-mode
+            // launch without frame_syn cannot exist
             if (mode == kModeKeys) {
                 a.synw = ws->synw;
                 a.zout = ws->zout;
                 QKD_HIP(launch_frame_syn(a, stream));
+            } else {
+                QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));
             }
             if (spec) {
                 int xdc = 0, sgrid = 0;
@@ -1560,8 +1605,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             }
             QKD_HIP(decoder_event(ws, stream));
             hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
-            QKD_HIP(hipGetLastError());
-            QKD_HIP(decoder_event(ws, stream));
+            QKD_HIP(decoder_event_close(ws, stream, hipGetLastError()));
             if (mode == kModeKeys) QKD_HIP(launch_key_match(a, stream));
             return QKD_OK;
         }
@@ -1597,8 +1641,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     }
     QKD_HIP(decoder_event(ws, stream));
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kDecodeBlock), lds, stream, a);
-    QKD_HIP(hipGetLastError());
-    QKD_HIP(decoder_event(ws, stream));
+    QKD_HIP(decoder_event_close(ws, stream, hipGetLastError()));
     return QKD_OK;
 }
 
@@ -1709,6 +1752,16 @@ qkd_status qkd_decode_batch(const qkd_code* c, qkd_workspace* ws, const double* 
 }
 
 
+// The speculation policy's per-QBER record (qkd_workspace::spec_clean). The
+// map is bounded: a workspace fed ever new QBERs (a continuous-q pipeline, a
+// sweep) forgets the records once there are kSpecCleanMax of them, which only
+// resamples those QBERs' replay fractions.
+static constexpr size_t kSpecCleanMax = 64;
+static SpecClean& spec_clean_of(qkd_workspace* ws, double q) {
+    if (ws->spec_clean.size() >= kSpecCleanMax && !ws->spec_clean.count(q)) ws->spec_clean.clear();
+    return ws->spec_clean[q];
+}
+
 // Shared by qkd_qkd_ldpc_batch and qkd_trials_batch: keys already packed in ws.
 static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_frames, double q,
                               uint32_t max_it, double thr, uint32_t flags, uint8_t* bits_out,
@@ -1762,8 +1815,8 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
         ws->spec_stat_pending = false;
         const bool over = (double)*ws->spec_stat_host > kSpecCkptSwitch * (double)ws->spec_stat_frames;
         if (over) ws->spec_ckpt_q = std::min(ws->spec_ckpt_q, ws->spec_stat_q);
-        int& cnt = ws->spec_clean[ws->spec_stat_q];
-        cnt = over ? 0 : cnt + 1;
+        SpecClean& sc = spec_clean_of(ws, ws->spec_stat_q);
+        sc.clean = over ? 0 : sc.clean + 1;
     }
     // at and above that QBER: the checkpointed speculation (QKD_CKPT_UNSAT
     // overrides its trigger; 0: exact iterations only)
@@ -1784,8 +1837,8 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     // only every kSpecStatEvery calls: each sample is a device-to-host copy
     // and an event on the caller's stream)
     {
-        auto& cnt = ws->spec_clean[q];
-        if (cnt >= 2 && (++ws->spec_skip % kSpecStatEvery) != 0) return st;
+        SpecClean& sc = spec_clean_of(ws, q);
+        if (sc.clean >= 2 && (++sc.skip % kSpecStatEvery) != 0) return st;
     }
     if (!ws->spec_stat_host) {
         if (hipHostMalloc(reinterpret_cast<void**>(&ws->spec_stat_host), 8, hipHostMallocDefault) != hipSuccess ||
@@ -2292,19 +2345,12 @@ qkd_status qkd_debug_decoder_timing(qkd_workspace* ws, int start, double* ms_tot
     if (!ws) return set_error(QKD_ERR_INVALID_ARG, "null workspace");
     DeviceGuard g(ws->device);
     std::lock_guard<std::mutex> lk(ws->mu);
-    double tot = 0.0;
-    const size_t pairs = ws->dec_ev_used / 2;
-    if (!start) {
-        for (size_t k = 0; k < pairs; ++k) {
-            QKD_HIP(hipEventSynchronize(ws->dec_ev[2 * k + 1]));
-            float ms = 0.0f;
-            QKD_HIP(hipEventElapsedTime(&ms, ws->dec_ev[2 * k], ws->dec_ev[2 * k + 1]));
-            tot += ms;
-        }
-    }
-    if (ms_total) *ms_total = tot;
-    if (launches) *launches = start ? 0 : pairs;
+    if (!start) QKD_HIP(decoder_events_fold(ws));
+    if (ms_total) *ms_total = start ? 0.0 : ws->dec_ms_folded;
+    if (launches) *launches = start ? 0 : ws->dec_pairs_folded;
     ws->dec_ev_used = 0;
+    ws->dec_ms_folded = 0.0;
+    ws->dec_pairs_folded = 0;
     ws->time_decoder = start != 0;
     return QKD_OK;
 }

@@ -96,6 +96,14 @@ struct DeviceCode {
 
 }  // namespace qkd
 
+// the speculation policy's record of one QBER (decode.hip decode_keys): clean =
+// consecutive replay samples under the switch; skip = calls since the last
+// sample once clean >= 2 (sampled every kSpecStatEvery calls)
+struct SpecClean {
+    int clean = 0;
+    uint64_t skip = 0;
+};
+
 struct qkd_workspace {
     const qkd_code* code = nullptr;
     int device = 0;
@@ -130,8 +138,7 @@ struct qkd_workspace {
     double spec_ckpt_q = 2.0;
     // per QBER: consecutive samples under the switch (decode_keys samples a
     // QBER with two such samples only every kSpecStatEvery calls)
-    std::map<double, int> spec_clean;
-    uint64_t spec_skip = 0;
+    std::map<double, SpecClean> spec_clean;
     // checkpointed speculation: one saved message store per resident workgroup
     double* ckpt = nullptr;
     size_t ckpt_slots = 0;
@@ -140,6 +147,8 @@ struct qkd_workspace {
     bool time_decoder = false;
     std::vector<hipEvent_t> dec_ev;        // start, stop, start, stop, ...
     size_t dec_ev_used = 0;
+    double dec_ms_folded = 0.0;            // finished pairs folded in (pool bound)
+    uint64_t dec_pairs_folded = 0;
 };
 
 struct qkd_code {

@@ -330,6 +330,9 @@ QKD_RHD void jump_poly_apply(const uint64_t p[4], uint64_t s[4]) {
     uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     uint64_t t[4] = {s[0], s[1], s[2], s[3]};
 #if defined(__HIP_DEVICE_COMPILE__)
+#if !defined(__gfx950__)
+#error "qkd_rng.h: the device jump uses gfx950's v_bitop3_b32; build with --offload-arch=gfx950"
+#endif
     // gfx950: a coefficient's mask is one sign-extended bit field extract
     // (v_bfe_i32), and each 32-bit half of a ^= t & m one v_bitop3_b32 (truth
     // table f(a, t, m) = a ^ (t & m) = 0xF0 ^ (0xCC & 0xAA) = 0x78)

@@ -57,6 +57,42 @@ def allreduce_counters(counters, group=None):
     return counters
 
 
+def run_sharded_point(rank: int, world: int, frames: int, run_shard, sync=None):
+    """One QBER point of `frames` trials sharded over the ranks (BASELINE configs[3]:
+    the reference's thread-pool fan-out of a point, simulation.cpp:230-250, and its
+    reduction, :252-312).
+
+    run_shard(begin, end) runs this rank's frames [begin, end) of the shared seed
+    stream and returns its qkd_counters record (uint8 tensor, 48 bytes, on the
+    rank's device). It is called twice: once untimed (allocation, clocks), then
+    timed between a barrier + sync() on both sides. The records are all-reduced
+    (SUM / MIN / MAX) and the time is the max over ranks. Every rank must call
+    this (it issues collectives when world > 1). Returns (counters, seconds,
+    (begin, end))."""
+    import torch
+    import torch.distributed as dist
+
+    sync = sync or (lambda: None)
+    b, e = shard_range(rank, world, frames)
+    run_shard(b, e)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    counters = run_shard(b, e)
+    sync()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        allreduce_counters(counters)
+        t = torch.tensor([dt], dtype=torch.float64, device=counters.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return counters, dt, (b, e)
+
+
 def free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -4,6 +4,9 @@ spawn_ranks -> init_rank -> shard_range -> allreduce_counters) over gloo on CPU,
 with each rank's frames decoded by the oracle (test infrastructure; the GPU
 path's own run is tests/test_dist_gpu.py). Usage (as a spawned rank):
     python tests/dist_rehearsal.py OUT_JSON FRAMES QBER [FAIL_RANK]
+With QKD_REHEARSAL=point the ranks run bench.py's configs[3] path instead
+(qkd_ldpc_amd.dist.run_sharded_point: untimed + timed shard runs, counter
+all-reduce, max-rank time), the oracle decoding each shard.
 """
 import json
 import os
@@ -33,16 +36,31 @@ def main():
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", "code_n10240.npz")))
     code = O.Code.from_lists(g)
     seeds = O.seeds(777, frames)
-    b, e = shard_range(rank, world, frames)
-    r = code.trials(q, seeds[b:e], 0, 50, 100.0, True, threads=2)
-    rec = torch.from_numpy(counters_of(np.asarray(r["iters"], np.uint32), np.asarray(r["sp_ok"], np.uint8),
-                                       np.asarray(r["key_ok"], np.uint8)))
-    allreduce_counters(rec)
-    t = torch.tensor([float(e - b)], dtype=torch.float64)
-    dist.all_reduce(t)
+    if os.environ.get("QKD_REHEARSAL") == "point":
+        from qkd_ldpc_amd.dist import run_sharded_point
+
+        def run_shard(b, e):
+            r = code.trials(q, seeds[b:e], 0, 50, 100.0, True, threads=2)
+            return torch.from_numpy(counters_of(np.asarray(r["iters"], np.uint32),
+                                                np.asarray(r["sp_ok"], np.uint8),
+                                                np.asarray(r["key_ok"], np.uint8)))
+
+        rec, dt, (b, e) = run_sharded_point(rank, world, frames, run_shard)
+        t = torch.tensor([float(e - b)], dtype=torch.float64)
+        dist.all_reduce(t)
+        extra = {"seconds": dt}
+    else:
+        b, e = shard_range(rank, world, frames)
+        r = code.trials(q, seeds[b:e], 0, 50, 100.0, True, threads=2)
+        rec = torch.from_numpy(counters_of(np.asarray(r["iters"], np.uint32), np.asarray(r["sp_ok"], np.uint8),
+                                           np.asarray(r["key_ok"], np.uint8)))
+        allreduce_counters(rec)
+        t = torch.tensor([float(e - b)], dtype=torch.float64)
+        dist.all_reduce(t)
+        extra = {}
     if rank == 0:
         with open(out, "w") as f:
-            json.dump({"world": world, "counters": rec.numpy().tolist(), "frames": t.item()}, f)
+            json.dump({"world": world, "counters": rec.numpy().tolist(), "frames": t.item(), **extra}, f)
     dist.destroy_process_group()
 
 

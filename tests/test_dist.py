@@ -120,3 +120,29 @@ def test_bench_gpus_two_without_gpus_fails_loudly():
     p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
     assert p.returncode != 0
     assert "no visible GPU" in p.stderr
+
+
+def test_config4_point_over_two_ranks_matches_fixture(tmp_path):
+    """bench.py's configs[3] path (dist.run_sharded_point) on two gloo ranks, the oracle
+    decoding each rank's shard of the first 40 config-4 frames: the all-reduced record
+    equals the config-4 fixture's counters over the same frames (bench.py
+    config4_fixture_counters), and the time is reported."""
+    import json
+    import sys
+    from qkd_ldpc_amd.dist import spawn_ranks
+    sys.path.insert(0, ROOT)
+    from bench import config4_fixture_counters
+    out = str(tmp_path / "c4.json")
+    frames = 40
+    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "dist_rehearsal.py"), out, str(frames), "0.02"],
+                     env_extra={"QKD_REHEARSAL": "point"})
+    assert rc == 0
+    got = json.load(open(out))
+    rec = np.array(got["counters"], np.uint8)
+    sums = rec[:40].view(np.uint64)
+    ext = rec[40:48].view(np.uint32)
+    want = config4_fixture_counters(frames)
+    assert got["frames"] == frames and got["seconds"] > 0
+    assert [int(x) for x in sums] == [want["frames"], want["sp_ok"], want["ldpc_ok"], want["sum_iters"],
+                                      want["sum_iters_sq"]]
+    assert [int(ext[0]), int(ext[1])] == [want["min_iters"], want["max_iters"]]

@@ -49,3 +49,25 @@ def test_bench_starts_its_own_ranks(golden_vectors):
     assert out["sum_iterations"] == int(it[sp].sum())
     assert out["fer"] == 0.0
     assert abs(out["value"] - 2 * 512 * 10240 * 2 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 1e-6
+
+
+def test_bench_config4_over_two_ranks():
+    """BASELINE configs[3] through `python bench.py --gpus 2` (two ranks on the one
+    MI355X over gloo): each rank runs its shard of the first 20,000 config-4 frames in
+    one qkd_trials_batch, the counters are all-reduced, and the `config4` block's
+    aggregate equals the oracle fixture's (tests/golden/config4_1m.npz) exactly."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["QKD_DIST_BACKEND"] = "gloo"
+    frames = 20000
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--prewarm-ms", "0", "--frames", "256", "--no-e2e", "--no-variants",
+                        "--no-cpu-baseline", "--config4-frames", str(frames)],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, p.stdout
+    c4 = json.loads(line[0])["config4"]
+    assert c4["n_gpus"] == 2 and c4["frames"] == frames and c4["frames_per_rank"] == frames // 2
+    assert c4["matches_fixture"] is True, c4["counters"]
+    assert c4["counters"]["frames"] == frames and c4["fer"] == 0.0
+    assert abs(c4["value"] - frames * 10240 / (c4["ms"] / 1e3)) / c4["value"] < 1e-9

@@ -415,3 +415,76 @@ def test_qkd_ldpc_unaligned_key_bytes(Q, H, golden_vectors):
     assert (r.iterations.cpu().numpy() == golden_vectors["c2_iters"][:64]).all()
     assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c2_ko"][:64]).all()
     assert (r.bits.cpu().numpy() == a.cpu().numpy()).all()
+
+
+def _chain_code(Q, n):
+    """H of the chain code (check j = bits j, j + 1), from check lists (a dense
+    array of N ~ 70,000 would take gigabytes)."""
+    co = (2 * np.arange(n, dtype=np.int32))
+    ci = np.stack([np.arange(n - 1), np.arange(1, n)], 1).reshape(-1).astype(np.int32)
+    return Q.HMatrix.from_check_lists(n, co, ci)
+
+
+@pytest.mark.parametrize("mode", ["fast", "replay"])
+def test_keygen_beyond_65536_bits(Q, oracle_mod, monkeypatch, mode):
+    """The two-wave generator at and past N = 65536, where its Lemire products leave
+    32 bits (keygen_split_kernel<false>: binary64 quotients, 64-bit draw indices),
+    and its serial regeneration path there: keys and exact QBER equal run_trial's."""
+    if mode != "fast":
+        monkeypatch.setenv("QKD_KEYGEN", mode)
+    rng = np.random.default_rng(65)
+    for n, q in [(65536, 0.02), (65536, 0.05), (65537, 0.02), (70001, 0.03)]:
+        H = _chain_code(Q, n)
+        seeds = rng.integers(0, 2**63, 3, dtype=np.int64).astype(np.uint64)
+        a, b, qq = Q.keygen(H, seeds_dev(seeds), q)
+        torch.cuda.synchronize()
+        a, b, qq = a.cpu().numpy(), b.cpu().numpy(), qq.cpu().numpy()
+        for f, s in enumerate(seeds):
+            wa, wb, wq = oracle_mod.keygen(int(s), n, q)
+            assert (a[f] == wa).all() and (b[f] == wb).all(), (mode, n, q, f)
+            assert qq[f] == wq
+
+
+def test_trials_beyond_65536_bits(Q, oracle_mod, tmp_path):
+    """run_trials on a 70,001-bit code (past the split decoder's N limit: the classic
+    kernel, with the binary64-quotient key generator): per-frame iterations and flags
+    equal the oracle's."""
+    from conftest import write_alist
+    n = 70001
+    H = _chain_code(Q, n)
+    cptr, cidx, bptr, bidx = H.adjacency()
+    p = str(tmp_path / "chain.alist")
+    write_alist(p, n, n - 1, bptr, bidx, cptr, cidx, pad=False)
+    oc = oracle_mod.Code.from_alist(p)
+    seeds = oracle_mod.seeds(70, 4)
+    for q, max_it in [(0.001, 6), (0.02, 4)]:
+        r = Q.run_trials(H, seeds_dev(seeds), q, 0, max_it, 100.0, True)
+        torch.cuda.synchronize()
+        want = oc.trials(q, seeds, 0, max_it, 100.0, True, threads=4)
+        assert (r.iterations.cpu().numpy() == want["iters"]).all(), q
+        assert (r.syndromes_match.cpu().numpy().astype(bool) == want["sp_ok"]).all()
+        assert (r.keys_match.cpu().numpy().astype(bool) == want["key_ok"]).all()
+
+
+def test_decoder_timing_counts_launches(Q, golden_code):
+    """qkd_debug_decoder_timing (the bench's live kernel time): pairs of HIP events
+    around each decoder launch; 600 calls cross the pool's fold point (256 pairs) and
+    every launch is counted once, with a positive total."""
+    import ctypes as C
+    g = golden_code
+    H = Q.HMatrix.from_check_lists(int(g["dims"][0]), g["chk_off"], g["chk_idx"])
+    ws = Q.Workspace(H)
+    seeds = seeds_dev(Q.make_seeds(777, 64))
+    alice, bob, q = Q.keygen(H, seeds, 0.02, 0, workspace=ws)
+    L = Q._native.lib()
+    tot, n = C.c_double(0), C.c_uint64(0)
+    Q._native.check(L.qkd_debug_decoder_timing(ws.handle, 1, C.byref(tot), C.byref(n)))
+    for k in range(600):
+        Q.qkd_ldpc(H, alice, bob, float(q[0].item()), workspace=ws)
+    Q._native.check(L.qkd_debug_decoder_timing(ws.handle, 0, C.byref(tot), C.byref(n)))
+    assert n.value == 600 and tot.value > 0
+    # off again: no events recorded, nothing counted
+    Q.qkd_ldpc(H, alice, bob, float(q[0].item()), workspace=ws)
+    Q._native.check(L.qkd_debug_decoder_timing(ws.handle, 0, C.byref(tot), C.byref(n)))
+    assert n.value == 0 and tot.value == 0.0
+    ws.close()
