@@ -1532,7 +1532,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             if (const char* g = getenv("QKD_DECODE_GRID")) grid = std::max(1, std::min(grid, atoi(g)));
             s = ws_reserve_decode(ws, (size_t)grid);
             if (s != QKD_OK) return s;
-            a.code = c->view();
+            a.code = c->view_split();     // the internal bit order (host.cpp build_code)
             a.c2b = ws->c2b;
             a.plan_enc = nullptr;
             if (rule == kRuleSp64) {

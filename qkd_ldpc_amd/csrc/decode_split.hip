@@ -404,7 +404,7 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
             for (int k = 0; k < kDvUnroll; ++k) jc[k] = (int32_t)(bc[u] >> (16 * k)) & 0xffff;
             const uint32_t bob = (uint32_t)(bobmask >> r) & 1u;
             float acc;
-            if constexpr (MODE == kModeLlr) acc = ok ? (float)a.llr[(size_t)f * c.n + i] : 0.0f;
+            if constexpr (MODE == kModeLlr) acc = ok ? (float)a.llr[(size_t)f * c.n + c.perm[i]] : 0.0f;
             else acc = bob ? -llr_p : llr_p;
             if (FOLD) {
                 const uint32_t sgi = bob ^ lsign;
@@ -808,7 +808,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 bo[2] = qkds::psi_of_exact(clamp_msg(acc - cv[2], a.thr));
             } else {
                 f2 L;
-                if constexpr (MODE == kModeLlr) L = qkds::iv_of(ok ? a.llr[(size_t)f * c.n + i] : 0.0);
+                if constexpr (MODE == kModeLlr) L = qkds::iv_of(ok ? a.llr[(size_t)f * c.n + c.perm[i]] : 0.0);
                 else L = bob ? f2{-a.lp_up, -a.lp_dn} : f2{a.lp_dn, a.lp_up};
                 f2 cs[kDvUnroll];
                 f2 T = L;
@@ -1040,23 +1040,28 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             }
             __syncthreads();
         }
-        // Bob's bits of this thread's bit-phase rounds (round r: bit tid + r *
-        // kDecodeBlock; N <= 64 * kDecodeBlock, kMaxBitsSplit). Without the fold
-        // the first check phase reads b2c = LLR_i (:188) from every slot.
+        // Bob's bits of this thread's bit-phase rounds (round r: internal bit
+        // q = tid + r * kDecodeBlock, original bit c.perm[q]; N <= 64 *
+        // kDecodeBlock, kMaxBitsSplit), and Alice's for the key compare at the
+        // frame's end. Without the fold the first check phase reads b2c = LLR_i
+        // (:188) from every slot.
         // (the speculative kernel's replay policy for this frame: ctl[6])
         const bool spec0 = SPEC == 1 && ctl[6] != 0;
         uint64_t bobmask = 0;
+        uint64_t alicemask = 0;
         // the first check phase's b2c = LLR_i in every slot (:188), as enclosing
         // intervals when speculating (the LLR path has no folded first iteration)
         auto init_slots = [&](bool as_interval) {
             int r = 0;
             for (int i = tid; i < c.n; i += kDecodeBlock, ++r) {
                 T l;
+                const int o = c.perm[i];
                 if (MODE == kModeLlr) {
-                    l = (T)a.llr[(size_t)f * c.n + i];
+                    l = (T)a.llr[(size_t)f * c.n + o];
                 } else {
-                    const uint32_t bb = (uint32_t)((bw[i >> 6] >> (i & 63)) & 1u);
+                    const uint32_t bb = (uint32_t)((bw[o >> 6] >> (o & 63)) & 1u);
                     bobmask |= (uint64_t)bb << r;
+                    if (a.key_ok) alicemask |= ((a.alice_w[(size_t)f * a.words + (o >> 6)] >> (o & 63)) & 1ull) << r;
                     l = bb ? -llr_p : llr_p;
                 }
                 if (!fold1) {
@@ -1209,7 +1214,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     const bool ok = i < c.n;
                     const int deg = dg[u];
                     T acc;
-                    if (MODE == kModeLlr) acc = ok ? (T)a.llr[(size_t)f * c.n + i] : (T)0;
+                    if (MODE == kModeLlr) acc = ok ? (T)a.llr[(size_t)f * c.n + c.perm[i]] : (T)0;
                     else acc = ((uint32_t)(bobmask >> r) & 1u) ? -llr_p : llr_p;
                     if constexpr (FOLDS) if (folded && ok) {
                         // fold_first_message: message of the k-th check j of bit i is
@@ -1373,13 +1378,12 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // (block-wide OR through ctl[7], no static LDS: the dynamic
             // allocation may take the whole 160 KB)
             if (a.key_ok) {
-                // (Alice's word read here rather than held in registers
-                // through the frame's iterations)
+                // this thread's bits of the last hard decision (zw, internal
+                // order) against Alice's (alicemask, from the prologue)
                 bool mis = false;
-                if (tid < (int)a.words) {
-                    uint64_t d = zw[tid] ^ a.alice_w[(size_t)f * a.words + tid];
-                    if ((tid + 1) * 64 > c.n) d &= (1ull << (c.n - tid * 64)) - 1ull;
-                    mis = d != 0;
+                for (int r = 0; r * kDecodeBlock < c.n; ++r) {
+                    const int q = tid + r * kDecodeBlock;
+                    if (q < c.n) mis |= ((zw[q >> 6] >> (q & 63)) ^ (alicemask >> r)) & 1ull;
                 }
                 if (__any(mis) && lane == 0) atomicOr(ctl + 7, 1u);
                 __syncthreads();
@@ -1388,12 +1392,13 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
                     ctl[7] = 0;
                 }
             }
-            // the packed decision for bits_out (zout_unpack_kernel)
+            // the packed decision for bits_out, internal order
+            // (zout_unpack_kernel puts the bits back in place)
             if (a.bits_out)
                 for (int q = tid; q < (int)a.words; q += kDecodeBlock) a.zout[(size_t)f * a.words + q] = zw[q];
         } else if (a.bits_out) {
             for (int i = tid; i < c.n; i += kDecodeBlock)
-                a.bits_out[(size_t)f * c.n + i] = (uint8_t)((zw[i >> 6] >> (i & 63)) & 1u);
+                a.bits_out[(size_t)f * c.n + c.perm[i]] = (uint8_t)((zw[i >> 6] >> (i & 63)) & 1u);
         }
         if (tid == 0) {
             a.iters[f] = done ? it + 1 : a.max_it;
@@ -1487,13 +1492,15 @@ __global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, cons
     }
 }
 
-__global__ void zout_unpack_kernel(const uint64_t* zout, uint32_t n, uint32_t words, uint32_t n_frames,
-                                   uint8_t* out) {
+// bits_out[f][bit] from the decoder's packed decisions in the internal bit
+// order (DeviceCode::inv)
+__global__ void zout_unpack_kernel(const uint64_t* zout, const int32_t* inv, uint32_t n, uint32_t words,
+                                   uint32_t n_frames, uint8_t* out) {
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (size_t)n_frames * n) return;
     const size_t f = gid / n;
-    const uint32_t i = (uint32_t)(gid - f * n);
-    out[gid] = (uint8_t)((zout[f * words + (i >> 6)] >> (i & 63)) & 1u);
+    const uint32_t q = (uint32_t)inv[gid - f * n];
+    out[gid] = (uint8_t)((zout[f * words + (q >> 6)] >> (q & 63)) & 1u);
 }
 
 hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
@@ -1510,7 +1517,7 @@ hipError_t launch_key_match(const DecodeArgs& a, hipStream_t stream) {
     if (a.bits_out) {
         const size_t total = (size_t)a.n_frames * a.code.n;
         hipLaunchKernelGGL(zout_unpack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, a.zout,
-                           (uint32_t)a.code.n, a.words, a.n_frames, a.bits_out);
+                           a.code.inv, (uint32_t)a.code.n, a.words, a.n_frames, a.bits_out);
     }
     return hipGetLastError();
 }

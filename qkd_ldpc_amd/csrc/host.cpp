@@ -46,6 +46,12 @@ static void free_device(qkd_code* c) {
     if (c->d_bit_code) (void)hipFree(c->d_bit_code);
     c->d_bit_code = nullptr;
     if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
+    for (void* p : {(void*)c->d_perm, (void*)c->d_inv, (void*)c->d_bit_chk_s, (void*)c->d_bit_deg_s,
+                    (void*)c->d_bit_pat_s})
+        if (p) (void)hipFree(p);
+    c->d_perm = c->d_inv = c->d_bit_chk_s = nullptr;
+    c->d_bit_deg_s = nullptr;
+    c->d_bit_pat_s = nullptr;
     c->d_bit_pat = nullptr;
     c->d_pat_deg = nullptr;
     if (c->d_plan) (void)hipFree(c->d_plan);
@@ -204,19 +210,70 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
                           hipMemcpyHostToDevice));
         QKD_HIP(hipMemcpy(c->d_pat_deg, c->pat_deg.data(), c->pat_deg.size(), hipMemcpyHostToDevice));
     }
-    // packed per-bit words for the speculative bit phases (qkd_internal.h)
+    // The split kernels' internal bit order (decode_split.hip): bits numbered
+    // in the order the check-phase plan meets their LAST edge (row deg - 1),
+    // task by task, lane by lane. Each task's last-row edges then have
+    // consecutive internal bits, and so consecutive message slots
+    // (row * n_pad + bit): the last row is the one the split store keeps in
+    // global memory, so a check phase's global accesses come in runs of
+    // whole lines instead of one line per edge, while the bit phase, which
+    // walks the internal order, stays coalesced. perm[internal] = bit,
+    // inv[bit] = internal; bits without edges go last.
+    std::vector<int32_t> perm(n), inv(n, -1);
+    {
+        int32_t nx = 0;
+        for (size_t k = 0; k < (size_t)plan.n_tasks * 64; ++k) {
+            const uint32_t b = plan.word[k] & qkdp::kPlanBitMask;
+            if (b < (uint32_t)n && (int32_t)(plan.word[k] >> 24) == bdeg[b] - 1 && inv[b] < 0) {
+                inv[b] = nx;
+                perm[nx++] = (int32_t)b;
+            }
+        }
+        for (int32_t i = 0; i < n; ++i)
+            if (inv[i] < 0) {
+                inv[i] = nx;
+                perm[nx++] = i;
+            }
+    }
+    // the per-bit arrays in that order (the split kernels' DeviceCode view)
+    std::vector<int32_t> bit_chk_s(bit_chk.size(), -1);
+    std::vector<uint8_t> bit_deg_s(n, 0);
+    for (int32_t q = 0; q < n; ++q) {
+        const int32_t b = perm[q];
+        bit_deg_s[q] = bit_deg[b];
+        for (int32_t k = 0; k < max_dv; ++k)
+            bit_chk_s[(size_t)k * c->n_pad + q] = bit_chk[(size_t)k * c->n_pad + b];
+    }
+    QKD_HIP(hipMalloc(&c->d_perm, (size_t)n * sizeof(int32_t)));
+    QKD_HIP(hipMemcpy(c->d_perm, perm.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice));
+    QKD_HIP(hipMalloc(&c->d_inv, (size_t)n * sizeof(int32_t)));
+    QKD_HIP(hipMemcpy(c->d_inv, inv.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice));
+    QKD_HIP(hipMalloc(&c->d_bit_chk_s, bit_chk_s.size() * sizeof(int32_t)));
+    QKD_HIP(hipMemcpy(c->d_bit_chk_s, bit_chk_s.data(), bit_chk_s.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    QKD_HIP(hipMalloc(&c->d_bit_deg_s, bit_deg_s.size()));
+    QKD_HIP(hipMemcpy(c->d_bit_deg_s, bit_deg_s.data(), bit_deg_s.size(), hipMemcpyHostToDevice));
+    if (c->n_pat > 0) {
+        std::vector<uint16_t> bit_pat_s(n);
+        for (int32_t q = 0; q < n; ++q) bit_pat_s[q] = bit_pat[perm[q]];
+        QKD_HIP(hipMalloc(&c->d_bit_pat_s, bit_pat_s.size() * sizeof(uint16_t)));
+        QKD_HIP(hipMemcpy(c->d_bit_pat_s, bit_pat_s.data(), bit_pat_s.size() * sizeof(uint16_t),
+                          hipMemcpyHostToDevice));
+    }
+    // packed per-bit words for the speculative bit phases (qkd_internal.h),
+    // split kernels only: in the internal order
     bool packable = m <= 65536 && max_dv <= 3;
     for (int32_t j = 0; j < m && packable; ++j) packable = chk_deg[j] >= 1 && chk_deg[j] <= 16;
     if (packable) {
         std::vector<uint64_t> code((size_t)c->n_pad, 0);
-        for (int32_t i = 0; i < n; ++i) {
+        for (int32_t q = 0; q < n; ++q) {
+            const int32_t i = perm[q];
             uint64_t w = (uint64_t)bdeg[i] << 48;
             for (int32_t k = 0; k < bdeg[i]; ++k) {
                 const int32_t j = bit_chk[(size_t)k * c->n_pad + i];
                 w |= (uint64_t)j << (16 * k);
                 w |= (uint64_t)(chk_deg[j] - 1) << (50 + 4 * k);
             }
-            code[i] = w;
+            code[q] = w;
         }
         QKD_HIP(hipMalloc(&c->d_bit_code, code.size() * sizeof(uint64_t)));
         QKD_HIP(hipMemcpy(c->d_bit_code, code.data(), code.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
@@ -225,9 +282,12 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     for (size_t k = 0; k < plan.word.size(); ++k) plan2[k] = make_uint2(plan.word[k], plan.seg[k]);
     QKD_HIP(hipMalloc(&c->d_plan, plan2.size() * sizeof(uint2)));
     QKD_HIP(hipMemcpy(c->d_plan, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    // the same plan slot-addressed (row * n_pad + bit; idle lanes: slot n)
-    for (size_t k = 0; k < plan.word.size(); ++k)
-        plan2[k].x = (plan.word[k] >> 24) * (uint32_t)c->n_pad + (plan.word[k] & qkdp::kPlanBitMask);
+    // the same plan slot-addressed for the split kernels (row * n_pad +
+    // internal bit; idle lanes: the dummy column n's slot)
+    for (size_t k = 0; k < plan.word.size(); ++k) {
+        const uint32_t b = plan.word[k] & qkdp::kPlanBitMask;
+        plan2[k].x = (plan.word[k] >> 24) * (uint32_t)c->n_pad + (b < (uint32_t)n ? (uint32_t)inv[b] : b);
+    }
     QKD_HIP(hipMalloc(&c->d_plan_slot, plan2.size() * sizeof(uint2)));
     QKD_HIP(hipMemcpy(c->d_plan_slot, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
     c->plan_slot_host = std::move(plan2);

@@ -92,6 +92,13 @@ struct DeviceCode {
     // plan with the message slot row * n_pad + bit in place of {bit, row}
     // (split kernels: their message store is slot-addressed)
     const uint2* plan_slot;
+    // The split kernels' view (qkd_code::view_split) numbers bits in an
+    // internal order (host.cpp build_code): bit_chk, bit_deg, bit_pat,
+    // bit_code and plan_slot are indexed by internal bit q, whose original
+    // bit is perm[q]; inv[bit] = q. nullptr in the classic kernels' view
+    // (original order). bit_code and plan_slot exist in the internal order only.
+    const int32_t* perm;
+    const int32_t* inv;
 };
 
 }  // namespace qkd
@@ -176,6 +183,13 @@ struct qkd_code {
     uint16_t* d_bit_pat = nullptr;
     uint64_t* d_bit_code = nullptr;
     uint8_t* d_pat_deg = nullptr;
+    // the split kernels' internal bit order (DeviceCode::perm / inv) and the
+    // per-bit arrays in it
+    int32_t* d_perm = nullptr;
+    int32_t* d_inv = nullptr;
+    int32_t* d_bit_chk_s = nullptr;
+    uint8_t* d_bit_deg_s = nullptr;
+    uint16_t* d_bit_pat_s = nullptr;
     // parallel key generation (decode.hip: keygen_fast_kernel): lane l of a
     // frame's kKeygenLanes-lane slice starts at draw l * keygen_chunk;
     // d_jump[b] = T^(chunk * 2^b)
@@ -192,10 +206,17 @@ struct qkd_code {
     int cu_count = 0;
     qkd_workspace* default_ws = nullptr;
 
+    // the classic kernels' view (original bit order)
     qkd::DeviceCode view() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
-                               n_pat, d_bit_pat, d_pat_deg, d_bit_code, d_plan_slot};
+                               n_pat, d_bit_pat, d_pat_deg, nullptr, nullptr, nullptr, nullptr};
+    }
+    // the split kernels' view (internal bit order, DeviceCode::perm)
+    qkd::DeviceCode view_split() const {
+        return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
+                               d_chk_bits, d_chk_deg, d_plan, d_bit_chk_s, nullptr, d_bit_deg_s,
+                               n_pat, d_bit_pat_s, d_pat_deg, d_bit_code, d_plan_slot, d_perm, d_inv};
     }
 };
 

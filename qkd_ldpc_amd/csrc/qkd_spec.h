@@ -56,26 +56,30 @@ typedef float f2 __attribute__((ext_vector_type(2)));   // [lo, hi]; packed bina
 // The two series of phi_core, for a binary32 value or a packed pair (every
 // operation elementwise, so a pair's halves are bit for bit the scalar
 // results), in Horner's form:
-//   series_t(x) = 1 - x/2 + x^2/6 - ... + x^6/5040   (w = 1 - e^-x = x t, x < 0.35)
-//   series_h(s) = 1 + s/3 + s^2/5 + ... + s^6/13      (2 atanh(u) = 2u h, s = u^2)
-// (Estrin's scheme, depth 3 for two more operations each, measured 1.5 %
-// slower per config-2 batch: DESIGN.md §4.3.)
+//   series_t(x) ~ (1 - e^-x) / x            (w = 1 - e^-x = x t, x < 0.35)
+//   series_h(s) ~ atanh(sqrt s) / sqrt s    (2 atanh(u) = 2u h, s = u^2 <= e^-2)
+// Degree-4 near-minimax fits with binary32 coefficients
+// (tools/phi_poly_fit.py): at most 5.6e-8 / 7.2e-8 relative error including
+// the binary32 Horner evaluation, below the Taylor degree-6 forms they replaced
+// (6.0e-8 / 1.2e-7) with two operations fewer each; 2^-20 (kPhiRel) bounds
+// the whole evaluation, certified over every binary32 input on the GPU
+// (tests/test_spec.py::test_phi_bounds_exhaustive).
+// (Estrin's scheme, depth 2 for one more operation each, measured slower per
+// config-2 batch at degree 6: DESIGN.md §4.3.)
 template <typename V>
-__device__ __forceinline__ V poly6(V z, float c0, float c1, float c2, float c3, float c4, float c5, float c6) {
-    V p = __builtin_elementwise_fma(z, V(c6), V(c5));
-    p = __builtin_elementwise_fma(z, p, V(c4));
-    p = __builtin_elementwise_fma(z, p, V(c3));
+__device__ __forceinline__ V poly4(V z, float c0, float c1, float c2, float c3, float c4) {
+    V p = __builtin_elementwise_fma(z, V(c4), V(c3));
     p = __builtin_elementwise_fma(z, p, V(c2));
     p = __builtin_elementwise_fma(z, p, V(c1));
     return __builtin_elementwise_fma(z, p, V(c0));
 }
 template <typename V>
 __device__ __forceinline__ V series_t(V x) {
-    return poly6(x, 1.0f, -0.5f, 1.0f / 6.0f, -1.0f / 24.0f, 1.0f / 120.0f, -1.0f / 720.0f, 1.0f / 5040.0f);
+    return poly4(x, 1.0f, -0x1.ffffa6p-2f, 0x1.554208p-3f, -0x1.52ba68p-5f, 0x1.d9f3c2p-8f);
 }
 template <typename V>
 __device__ __forceinline__ V series_h(V s) {
-    return poly6(s, 1.0f, 1.0f / 3.0f, 0.2f, 1.0f / 7.0f, 1.0f / 9.0f, 1.0f / 11.0f, 1.0f / 13.0f);
+    return poly4(s, 1.0f, 0x1.55549p-2f, 0x1.9a05a2p-3f, 0x1.1b7792p-3f, 0x1.2e9afep-3f);
 }
 // phi (PSI: phi / ln 2) and an upper bound of |phi'(x)| = 1 / sinh(x)
 // (within a factor 2) at 0 < x <= kPhiHuge from u = e^-x (accurate) and x
@@ -88,8 +92,7 @@ struct PhiVal {
 template <bool PSI>
 __device__ __forceinline__ PhiVal phi_core(float x, float u) {
     // w = 1 - u: direct for x >= 0.35 (u <= 0.705: the subtraction costs under
-    // a bit), below it the series x (1 - x/2 + x^2/6 - ... + x^6/5040)
-    // (truncation < x^7 / 40320 < 1.7e-8 relative)
+    // a bit), below it x series_t(x) (5.6e-8 relative at most)
     // (series_t starts on x before u = e^-x is ready; the two series in one
     // packed evaluation, which waits for u, measured no faster)
     const float t = series_t(x);
@@ -102,8 +105,8 @@ __device__ __forceinline__ PhiVal phi_core(float x, float u) {
     // 1.5 ulp of the argument)
     const float lg = __builtin_amdgcn_logf(w2 * rw);
     const float vlo = PSI ? lg : kLn2 * lg;
-    // x >= 1: phi = 2 atanh(u) = 2u (1 + s/3 + s^2/5 + ... + s^6/13), s = u^2 <= e^-2
-    // (truncation < s^7 / 15 (1 + s) < 6.4e-8 relative, under 7 % of kPhiRel)
+    // x >= 1: phi = 2 atanh(u) = 2u series_h(s), s = u^2 <= e^-2 (7.2e-8
+    // relative at most, under 8 % of kPhiRel)
     const float s = u * u;
     const float h = series_h(s);
     const float vhi = (u * (PSI ? 2.0f * kInvLn2 : 2.0f)) * h;

@@ -25,3 +25,21 @@ import json;d=json.loads(open('$O/bench_$l.json').read().strip().splitlines()[-1
 print('$l', 'step', round(d['ms_per_step'],4), 'kernel', round(d['roofline']['kernel_ms'],4), 'call', round(d['roofline']['call_ms'],4), 'e2e', round(d['end_to_end']['ms_per_step'],4) if 'end_to_end' in d else '', 'replays', d['speculation']['replayed_frames'])"
   done
 done
+# PMC="WRITE_SIZE" (one counter group): per build, one rocprofv3 --pmc pass over a
+# short bench; the decode kernel's mean counter values per dispatch
+if [ -n "${PMC:-}" ]; then
+  for l in $LIBS; do
+    QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=$(libpath $l) timeout -s KILL 120 rocprofv3 --pmc $PMC --output-format csv \
+      -d $O/pmc_$l -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-e2e \
+      --no-sweeps > $O/pmc_$l.log 2>&1 || { echo "pmc $l failed"; tail $O/pmc_$l.log; exit 1; }
+    python3 - $O/pmc_$l $l <<'PY'
+import csv, glob, sys, collections
+v = collections.defaultdict(list)
+for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "decode" in r["Kernel_Name"]:
+            v[r["Counter_Name"]].append(float(r["Counter_Value"]))
+print(sys.argv[2], {k: round(sum(x) / len(x)) for k, x in v.items()})
+PY
+  done
+fi
