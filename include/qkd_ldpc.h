@@ -297,6 +297,18 @@ QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t 
  * reference counterpart (the reference has no speculative iterations). */
 QKD_API qkd_status qkd_debug_phi_sweep(int which, uint32_t first_bits, uint32_t last_bits, uint64_t *result);
 
+/* The split decoder's internal bit order of a code given as a check-side CSR
+ * (as qkd_code_create), computed on the host without a device: perm_out[q]
+ * (n_bits entries) = the original bit at internal position q; plan_out
+ * (optional, 64 * n_tasks entries, n_tasks from *n_tasks_out when plan_out is
+ * null) = the check-phase wave plan's first words (bit | row << 24, idle lanes
+ * bit = n_bits); mode: NULL for the shipped order, "runs" without its LDS bank
+ * pass, "identity". Test infrastructure (tests/test_bit_order.py, CPU); no
+ * reference counterpart. */
+QKD_API qkd_status qkd_debug_bit_order(int32_t n_bits, int32_t n_checks, const int32_t *check_ptr,
+                                       const int32_t *check_idx, const char *mode, int32_t *perm_out,
+                                       uint32_t *plan_out, int32_t *n_tasks_out);
+
 /* ---- host helpers --------------------------------------------------------- */
 /* seeds[k] = k-th raw xoshiro256++(simulation_seed) output (simulation.cpp:222-228). */
 QKD_API qkd_status qkd_make_seeds(uint64_t simulation_seed, size_t count, uint64_t *seeds_host);

@@ -63,7 +63,7 @@ EXPORTS = [
     "qkd_keygen_batch", "qkd_trials_batch", "qkd_counters_batch", "qkd_make_seeds",
     "qkd_qber_range", "qkd_debug_phase_cycles", "qkd_debug_spec_replays", "qkd_debug_math", "qkd_debug_phi_sweep", "qkd_trace_decode",
     "qkd_interactive_batch",
-    "qkd_code_from_alist_ex", "qkd_debug_decoder_timing",
+    "qkd_code_from_alist_ex", "qkd_debug_decoder_timing", "qkd_debug_bit_order",
 ]
 
 
@@ -130,6 +130,7 @@ def lib():
             "qkd_debug_spec_replays": (st, [P, P, C.c_int]),
             "qkd_debug_math": (st, [C.c_int, P, P, SZ, P]),
             "qkd_debug_phi_sweep": (st, [C.c_int, C.c_uint32, C.c_uint32, P]),
+            "qkd_debug_bit_order": (st, [I32, I32, P, P, C.c_char_p, P, P, C.POINTER(I32)]),
             "qkd_interactive_batch": (st, [P, P, C.c_uint64, SZ, P, C.c_uint32, C.c_double, C.c_uint32,
                                            P, P, P, P, P, P]),
             "qkd_trace_decode": (st, [P, P, P, U32, D, U32, P, P, P, P]),

@@ -945,15 +945,71 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
     __syncthreads();
 
     if (!shuffle_wave) {
+        // Alice's bits: cb is a multiple of 32 (host.cpp), so a lane's chunk
+        // is whole 32-bit words of the key, written by that lane alone. A
+        // block of 32 draws shifts each draw's top bit into a register from
+        // the right (one v_alignbit_b32) and reverses it at the end, so draw
+        // d lands on bit d & 31.
         const uint32_t first = l * cb;
         const uint32_t end = live ? min(first + cb, n) : first;
-        uint64_t acc = 0;
-        for (uint32_t d = first; d < end; ++d) {
-            acc |= (g.next() >> 63) << (d & 63u);
-            if ((d & 63u) == 63u || d + 1 == end) {
-                atomicOr(reinterpret_cast<unsigned long long*>(&aw[d >> 6]), (unsigned long long)acc);
-                acc = 0;
+        uint32_t* aw32 = reinterpret_cast<uint32_t*>(aw);
+        for (uint32_t d = first; d < end; d += 32) {
+            uint32_t acc = 0;
+            const uint32_t cnt = min(32u, end - d);
+            if (cnt == 32) {
+#pragma unroll 8
+                for (int k = 0; k < 32; ++k)
+                    acc = __builtin_amdgcn_alignbit(acc, (uint32_t)(g.next_fast() >> 32), 31);
+                aw32[d >> 5] = __builtin_bitreverse32(acc);
+            } else {
+                for (uint32_t k = 0; k < cnt; ++k)
+                    acc = __builtin_amdgcn_alignbit(acc, (uint32_t)(g.next_fast() >> 32), 31);
+                aw32[d >> 5] = __builtin_bitreverse32(acc) >> (32 - cnt);
             }
+        }
+    } else if constexpr (R32) {
+        // The shuffle's pair draws, N <= 65536: every range (i + 1)(i + 2) <
+        // 2^32 (kept up to date by one add per draw). Lemire's product r *
+        // range in 32-bit pieces: x = its high 64 bits is A_hi + carry(A_lo +
+        // B_hi) for A = r_hi * range, B = r_lo * range; its low 64 bits are
+        // below range (the rejection test, probability ~2^-32) only if A_lo +
+        // B_hi wraps to 0, and only then is B_lo needed. The pair split x /
+        // (i + 2) as a binary32 reciprocal product with one exact correction
+        // (checked on the host for every divisor), its remainder by a 24-bit
+        // multiply (q, i + 2 < 2^17).
+        uint64_t d = (uint64_t)n + (uint64_t)l * cs;
+        const uint64_t end = live ? min(d + cs, draws) : d;
+        if (d < end && d < pair0) {                      // the lone draw (even N): lane 0
+            s_lone[slot] = (uint32_t)(g.next_fast() >> 63);
+            ++d;
+        }
+        uint32_t i = i0 + 2u * (uint32_t)(d - pair0);
+        uint32_t rg = (i + 1u) * (i + 2u);
+        for (; d < end; ++d) {
+            const uint64_t r = g.next_fast();
+            const uint32_t rl = (uint32_t)r, rh = (uint32_t)(r >> 32);
+            const uint32_t alo = rh * rg, ahi = __umulhi(rh, rg), bhi = __umulhi(rl, rg);
+            const uint32_t t = alo + bhi;
+            const uint32_t x = ahi + (t < alo ? 1u : 0u);
+            if (t == 0u) {
+                const uint32_t blo = rl * rg;
+                if (blo < rg && (uint64_t)blo < (0ull - (uint64_t)rg) % (uint64_t)rg) s_reject[slot] = 1;
+            }
+            const uint32_t bb = i + 2u;
+            const uint32_t q0 = (uint32_t)((float)x * __builtin_amdgcn_rcpf((float)bb));
+            const int32_t r0 = (int32_t)(x - __umul24(q0, bb));
+            // (the correction as selects, no divergent branch)
+            const bool lo = r0 < 0, hi = r0 >= (int32_t)bb;
+            const uint32_t q = q0 + (hi ? 1u : 0u) - (lo ? 1u : 0u);
+            const int32_t rem = r0 + (lo ? (int32_t)bb : 0) - (hi ? (int32_t)bb : 0);
+            if (i < ne) {
+                park[(i - i0) >> 1] = make_uint2(q, (uint32_t)rem);
+            } else {
+                if (q < ne) atomicMax(&last[q], i);
+                if ((uint32_t)rem < ne) atomicMax(&last[rem], i + 1);
+            }
+            rg += 4u * i + 10u;                          // (i + 3)(i + 4)
+            i += 2u;
         }
     } else {
         const uint64_t first = (uint64_t)n + (uint64_t)l * cs;
@@ -968,23 +1024,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
             const uint64_t b1 = (uint64_t)i + 2;
             const uint64_t range = ((uint64_t)i + 1) * b1;
             uint32_t qa, qb;
-            if constexpr (R32) {
-                // (keygen_fast_kernel's 32-bit form)
-                const uint32_t rg = (uint32_t)range, bb = (uint32_t)b1;
-                const uint64_t p0 = (uint64_t)(uint32_t)r * rg;
-                const uint64_t p1 = (uint64_t)(uint32_t)(r >> 32) * rg;
-                const uint64_t lo = p0 + (p1 << 32);
-                if (lo < range) {
-                    if (lo < (0 - range) % range) s_reject[slot] = 1;
-                }
-                const uint32_t x = (uint32_t)((p1 + (p0 >> 32)) >> 32);
-                uint32_t q = (uint32_t)((float)x * __builtin_amdgcn_rcpf((float)bb));
-                int32_t rem = (int32_t)(x - q * bb);
-                if (rem < 0) { --q; rem += (int32_t)bb; }
-                else if (rem >= (int32_t)bb) { ++q; rem -= (int32_t)bb; }
-                qa = q;
-                qb = (uint32_t)rem;
-            } else {
+            {
                 const uint64_t lo = r * range;
                 if (lo < range && lo < (0 - range) % range) s_reject[slot] = 1;
                 const uint64_t x = qkdr::mul_hi64(r, range);
@@ -2181,7 +2221,7 @@ __global__ void phi_sweep_kernel(int which, uint32_t first, uint32_t last, unsig
         double S, v, lo, hi, sl;       // S in nep units; v, lo, hi in the form's output units
         if (which == 4) {
             const float a1 = __builtin_amdgcn_fmed3f(a, 0.0f, qkds::kPhiHuge);
-            const qkds::PhiVal e = qkds::phi_core<true>(a1, qkds::exp_neg(a1));
+            const qkds::PhiVal e = qkds::phi_core<true, false>(a1, qkds::exp_neg(a1), __builtin_amdgcn_logf(a1));
             const qkds::f2 b = qkds::phi_bounds(a, a);
             S = a1;
             v = e.v * 0.6931471805599453;         // psi -> phi
@@ -2190,7 +2230,8 @@ __global__ void phi_sweep_kernel(int which, uint32_t first, uint32_t last, unsig
             sl = e.slope;
         } else {
             const float at = __builtin_fminf(a, qkds::kPsiHuge);
-            const qkds::PhiVal e = qkds::phi_core<false>(at * qkds::kLn2, __builtin_amdgcn_exp2f(-at));
+            const qkds::PhiVal e = qkds::phi_core<false, true>(at * qkds::kLn2, __builtin_amdgcn_exp2f(-at),
+                                                               __builtin_amdgcn_logf(at));
             const qkds::f2 b = qkds::phi_bounds_out(a, a);
             S = (double)at * 0.6931471805599453;
             v = e.v;

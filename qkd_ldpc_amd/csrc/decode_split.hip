@@ -915,8 +915,15 @@ __device__ __forceinline__ uint32_t region_of_block() {
 // a.ckpt_unsat checks unsatisfied the message store is saved (a.ckpt) and
 // the iterations go on with intervals; a frame they cannot certify within
 // spec_cap iterations resumes exactly from the saved messages.
+// (experiment builds: QKD_SPLIT_WAVES_PER_EU=8 asks for two workgroups per
+// CU, 64 VGPRs; run with QKD_SPLIT_BUDGET halving the LDS. DESIGN.md §4.3)
+#ifdef QKD_SPLIT_WAVES_PER_EU
+#define QKD_SPLIT_BOUNDS __launch_bounds__(kDecodeBlock, QKD_SPLIT_WAVES_PER_EU)
+#else
+#define QKD_SPLIT_BOUNDS __launch_bounds__(kDecodeBlock)
+#endif
 template <int MODE, int RULE, int DC, bool CLAMP, int SPEC>
-__global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a) {
+__global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     using T = typename RuleMsg<RULE>::T;
     // QKD path: the first check phase folds into the first bit phase for both
     // sum-product rules (every b2c is +-log_p, so every message is +-C_d:
@@ -1026,7 +1033,8 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
         if (SPEC && tid == 0)
             launch_replays = __hip_atomic_load(a.replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-        // ---- prologue. Keys path: the frame's Bob words staged in LDS (the
+        // ---- prologue. Keys path: the frame's Bob words, in the internal
+        //      bit order (frame_syn_kernel permuted them), staged in LDS (the
         //      product rows are free until the first check phase) and its
         //      syndrome words from frame_syn_kernel.
         const uint64_t* bw = reinterpret_cast<const uint64_t*>(smem + L.tval);
@@ -1041,27 +1049,23 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             __syncthreads();
         }
         // Bob's bits of this thread's bit-phase rounds (round r: internal bit
-        // q = tid + r * kDecodeBlock, original bit c.perm[q]; N <= 64 *
-        // kDecodeBlock, kMaxBitsSplit), and Alice's for the key compare at the
-        // frame's end. Without the fold the first check phase reads b2c = LLR_i
-        // (:188) from every slot.
+        // i = tid + r * kDecodeBlock; N <= 64 * kDecodeBlock, kMaxBitsSplit).
+        // Without the fold the first check phase reads b2c = LLR_i (:188),
+        // i.e. the caller's LLR of bit c.perm[i], from every slot.
         // (the speculative kernel's replay policy for this frame: ctl[6])
         const bool spec0 = SPEC == 1 && ctl[6] != 0;
         uint64_t bobmask = 0;
-        uint64_t alicemask = 0;
         // the first check phase's b2c = LLR_i in every slot (:188), as enclosing
         // intervals when speculating (the LLR path has no folded first iteration)
         auto init_slots = [&](bool as_interval) {
             int r = 0;
             for (int i = tid; i < c.n; i += kDecodeBlock, ++r) {
                 T l;
-                const int o = c.perm[i];
                 if (MODE == kModeLlr) {
-                    l = (T)a.llr[(size_t)f * c.n + o];
+                    l = (T)a.llr[(size_t)f * c.n + c.perm[i]];
                 } else {
-                    const uint32_t bb = (uint32_t)((bw[o >> 6] >> (o & 63)) & 1u);
+                    const uint32_t bb = (uint32_t)((bw[i >> 6] >> (i & 63)) & 1u);
                     bobmask |= (uint64_t)bb << r;
-                    if (a.key_ok) alicemask |= ((a.alice_w[(size_t)f * a.words + (o >> 6)] >> (o & 63)) & 1ull) << r;
                     l = bb ? -llr_p : llr_p;
                 }
                 if (!fold1) {
@@ -1378,12 +1382,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
             // (block-wide OR through ctl[7], no static LDS: the dynamic
             // allocation may take the whole 160 KB)
             if (a.key_ok) {
-                // this thread's bits of the last hard decision (zw, internal
-                // order) against Alice's (alicemask, from the prologue)
+                // (Alice's word read here rather than held in registers
+                // through the frame's iterations; both words in the internal
+                // bit order)
                 bool mis = false;
-                for (int r = 0; r * kDecodeBlock < c.n; ++r) {
-                    const int q = tid + r * kDecodeBlock;
-                    if (q < c.n) mis |= ((zw[q >> 6] >> (q & 63)) ^ (alicemask >> r)) & 1ull;
+                if (tid < (int)a.words) {
+                    uint64_t d = zw[tid] ^ a.alice_w[(size_t)f * a.words + tid];
+                    if ((tid + 1) * 64 > c.n) d &= (1ull << (c.n - tid * 64)) - 1ull;
+                    mis = d != 0;
                 }
                 if (__any(mis) && lane == 0) atomicOr(ctl + 7, 1u);
                 __syncthreads();
@@ -1426,10 +1432,14 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_split_kernel(DecodeArgs a
 constexpr int kSynFrames = QKD_SYN_FRAMES;
 constexpr int kSynBlock = 256;
 constexpr int kSynRow = 8;
-__global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, const uint64_t* __restrict__ alice_w,
-                                                              const uint64_t* __restrict__ bob_w, uint32_t words,
-                                                              uint32_t n_frames, uint32_t lsign, uint32_t* synw,
-                                                              uint32_t* counter) {
+//
+// It also rewrites the frames' two keys in place in the split decoder's
+// internal bit order (DeviceCode::perm: internal bit q holds original bit
+// perm[q]), from the copies it staged: the decoder then reads Bob's bits and
+// compares Alice's word by word with no gathers of its own.
+__global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, uint64_t* alice_w, uint64_t* bob_w,
+                                                              uint32_t words, uint32_t n_frames, uint32_t lsign,
+                                                              uint32_t* synw, uint32_t* counter) {
     // [kSynFrames][2 * words] pairs (Alice's 32-bit word, Bob's 32-bit word):
     // one 8-byte LDS read gives both keys' bit
     extern __shared__ uint2 kw[];
@@ -1490,6 +1500,42 @@ __global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, cons
             }
         }
     }
+    // the keys in the internal order: word w of a frame gathers bits
+    // perm[64 w + lane] (one perm load serves the workgroup's frames). A wave
+    // takes kSynPermBatch consecutive words at a time, issues their perm loads
+    // first, and lane u keeps word u's ballots, so each key's words leave as
+    // one coalesced store per frame.
+    constexpr uint32_t kSynPermBatch = 8;
+    constexpr uint32_t NWS = kSynBlock / 64;
+    for (uint32_t w0 = (threadIdx.x >> 6) * kSynPermBatch; w0 < words; w0 += NWS * kSynPermBatch) {
+        uint32_t ob[kSynPermBatch];
+#pragma unroll
+        for (uint32_t u = 0; u < kSynPermBatch; ++u) {
+            const uint32_t q = (w0 + u) * 64 + (uint32_t)lane;
+            ob[u] = q < (uint32_t)c.n ? (uint32_t)c.perm[q] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int fr = 0; fr < kSynFrames; ++fr) {
+            uint64_t mya = 0, myb = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < kSynPermBatch; ++u) {
+                const bool in = ob[u] != 0xffffffffu;
+                const uint32_t o = in ? ob[u] : 0u;
+                const uint2 v = kw[fr * w32 + (o >> 5)];
+                const uint64_t am = __ballot(in && ((v.x >> (o & 31u)) & 1u));
+                const uint64_t bm = __ballot(in && ((v.y >> (o & 31u)) & 1u));
+                if ((uint32_t)lane == u) {
+                    mya = am;
+                    myb = bm;
+                }
+            }
+            const uint32_t w = w0 + (uint32_t)lane;
+            if ((uint32_t)lane < kSynPermBatch && w < words && (uint32_t)fr < nf) {
+                alice_w[(size_t)(f0 + fr) * words + w] = mya;
+                bob_w[(size_t)(f0 + fr) * words + w] = myb;
+            }
+        }
+    }
 }
 
 // bits_out[f][bit] from the decoder's packed decisions in the internal bit
@@ -1507,8 +1553,8 @@ hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
     const size_t lds = (size_t)kSynFrames * 2 * a.words * sizeof(uint64_t);
     hipLaunchKernelGGL(frame_syn_kernel, dim3((a.n_frames + kSynFrames - 1) / kSynFrames), dim3(kSynBlock), lds,
-                       stream, a.code, a.alice_w, a.bob_w, a.words, a.n_frames, lsign,
-                       const_cast<uint32_t*>(a.synw), a.counter);
+                       stream, a.code, const_cast<uint64_t*>(a.alice_w), const_cast<uint64_t*>(a.bob_w), a.words,
+                       a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter);
     return hipGetLastError();
 }
 

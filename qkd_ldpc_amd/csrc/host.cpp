@@ -72,6 +72,118 @@ static void free_device(qkd_code* c) {
     c->d_bit_deg = nullptr;
 }
 
+// The internal order's second pass (build_code): inside each task's run of
+// last-row bits the order is free (the run stays one run of slots), and it
+// decides the LDS banks of the OTHER rows' slots of those bits, which the
+// check phases read and write scattered: slot x = row * n_pad + bit sits in
+// the bank pair x mod 32 (8-byte slots over 64 four-byte banks), and a
+// half-wave's accesses serialise on the busiest pair. A deterministic local
+// search swaps bits within runs while the summed excess over the tasks'
+// half-waves (busiest pair's count - 1, not-last-row edges) does not grow
+// (tools/bank_model.py: 3.06 -> ~1.1 extra bank cycles per task for the
+// N = 10240 code).
+static void bank_balance_runs(int32_t n, int32_t n_pad, const std::vector<int32_t>& bdeg,
+                              const qkdp::WavePlan& plan, std::vector<int32_t>& perm, std::vector<int32_t>& inv) {
+    const int32_t n_tasks = plan.n_tasks;
+    std::vector<std::vector<int32_t>> tasks_of(n);
+    std::vector<std::vector<int32_t>> runs(n_tasks);
+    for (int32_t t = 0; t < n_tasks; ++t)
+        for (int l = 0; l < 64; ++l) {
+            const uint32_t w = plan.word[(size_t)t * 64 + l];
+            const uint32_t b = w & qkdp::kPlanBitMask;
+            if (b >= (uint32_t)n) continue;
+            if ((int32_t)(w >> 24) == bdeg[b] - 1) runs[t].push_back((int32_t)b);
+            if (tasks_of[b].empty() || tasks_of[b].back() != t) tasks_of[b].push_back(t);
+        }
+    // (the edges of a task are distinct slots; idle lanes are skipped)
+    auto cost = [&](int32_t t) {
+        int ex = 0;
+        for (int h = 0; h < 2; ++h) {
+            int cnt[32] = {0};
+            for (int l = h * 32; l < h * 32 + 32; ++l) {
+                const uint32_t w = plan.word[(size_t)t * 64 + l];
+                const uint32_t b = w & qkdp::kPlanBitMask;
+                const int32_t row = (int32_t)(w >> 24);
+                if (b >= (uint32_t)n || row == bdeg[b] - 1) continue;
+                cnt[((uint32_t)row * (uint32_t)n_pad + (uint32_t)inv[b]) & 31u]++;
+            }
+            int mx = 0;
+            for (int k = 0; k < 32; ++k) mx = std::max(mx, cnt[k]);
+            ex += mx > 0 ? mx - 1 : 0;
+        }
+        return ex;
+    };
+    std::vector<int> cur(n_tasks);
+    for (int32_t t = 0; t < n_tasks; ++t) cur[t] = cost(t);
+    uint64_t rng = 0x9e3779b97f4a7c15ull;
+    auto next = [&]() {
+        rng ^= rng << 13;
+        rng ^= rng >> 7;
+        rng ^= rng << 17;
+        return rng;
+    };
+    const int64_t iters = std::min<int64_t>(200000, (int64_t)20 * n);
+    std::vector<int32_t> aff;
+    std::vector<int> nc;
+    for (int64_t it = 0; it < iters; ++it) {
+        const auto& run = runs[next() % (uint64_t)n_tasks];
+        if (run.size() < 2) continue;
+        const int32_t a = run[next() % run.size()], b = run[next() % run.size()];
+        if (a == b) continue;
+        aff.clear();
+        for (int32_t t : tasks_of[a]) aff.push_back(t);
+        for (int32_t t : tasks_of[b]) aff.push_back(t);
+        std::sort(aff.begin(), aff.end());
+        aff.erase(std::unique(aff.begin(), aff.end()), aff.end());
+        int before = 0;
+        for (int32_t t : aff) before += cur[t];
+        std::swap(inv[a], inv[b]);
+        int after = 0;
+        nc.resize(aff.size());
+        for (size_t k = 0; k < aff.size(); ++k) after += nc[k] = cost(aff[k]);
+        if (after <= before) {
+            for (size_t k = 0; k < aff.size(); ++k) cur[aff[k]] = nc[k];
+        } else {
+            std::swap(inv[a], inv[b]);
+        }
+    }
+    for (int32_t i = 0; i < n; ++i) perm[inv[i]] = i;
+}
+
+// The split kernels' internal bit order (decode_split.hip, DeviceCode::perm):
+// bits numbered in the order the check-phase plan meets their LAST edge (row
+// deg - 1), task by task, lane by lane. Each task's last-row edges then have
+// consecutive internal bits, and so consecutive message slots (row * n_pad +
+// bit): the last row is the one the split store keeps in global memory, so a
+// check phase's global accesses come in runs of whole lines instead of one
+// line per edge, while the bit phase, which walks the internal order, stays
+// coalesced. Then bank_balance_runs orders each run for the LDS banks.
+// perm[internal] = bit, inv[bit] = internal; bits without edges go last.
+// mode (diagnostics, QKD_BIT_ORDER): "identity" keeps the original order,
+// "runs" skips the bank pass.
+static void internal_bit_order(int32_t n, int32_t n_pad, const std::vector<int32_t>& bdeg,
+                               const qkdp::WavePlan& plan, std::vector<int32_t>& perm, std::vector<int32_t>& inv,
+                               const char* mode) {
+    int32_t nx = 0;
+    for (size_t k = 0; k < (size_t)plan.n_tasks * 64; ++k) {
+        const uint32_t b = plan.word[k] & qkdp::kPlanBitMask;
+        if (b < (uint32_t)n && (int32_t)(plan.word[k] >> 24) == bdeg[b] - 1 && inv[b] < 0) {
+            inv[b] = nx;
+            perm[nx++] = (int32_t)b;
+        }
+    }
+    for (int32_t i = 0; i < n; ++i)
+        if (inv[i] < 0) {
+            inv[i] = nx;
+            perm[nx++] = i;
+        }
+    if (mode && !strcmp(mode, "identity")) {
+        for (int32_t i = 0; i < n; ++i) perm[i] = inv[i] = i;
+    } else if (!(mode && !strcmp(mode, "runs"))) {
+        bank_balance_runs(n, n_pad, bdeg, plan, perm, inv);
+    }
+}
+
 // Validate the check-side CSR, derive the bit side, upload the ELL layouts.
 static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* cptr,
                              const int32_t* cidx, int device) {
@@ -210,31 +322,9 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
                           hipMemcpyHostToDevice));
         QKD_HIP(hipMemcpy(c->d_pat_deg, c->pat_deg.data(), c->pat_deg.size(), hipMemcpyHostToDevice));
     }
-    // The split kernels' internal bit order (decode_split.hip): bits numbered
-    // in the order the check-phase plan meets their LAST edge (row deg - 1),
-    // task by task, lane by lane. Each task's last-row edges then have
-    // consecutive internal bits, and so consecutive message slots
-    // (row * n_pad + bit): the last row is the one the split store keeps in
-    // global memory, so a check phase's global accesses come in runs of
-    // whole lines instead of one line per edge, while the bit phase, which
-    // walks the internal order, stays coalesced. perm[internal] = bit,
-    // inv[bit] = internal; bits without edges go last.
+    // the split kernels' internal bit order (internal_bit_order)
     std::vector<int32_t> perm(n), inv(n, -1);
-    {
-        int32_t nx = 0;
-        for (size_t k = 0; k < (size_t)plan.n_tasks * 64; ++k) {
-            const uint32_t b = plan.word[k] & qkdp::kPlanBitMask;
-            if (b < (uint32_t)n && (int32_t)(plan.word[k] >> 24) == bdeg[b] - 1 && inv[b] < 0) {
-                inv[b] = nx;
-                perm[nx++] = (int32_t)b;
-            }
-        }
-        for (int32_t i = 0; i < n; ++i)
-            if (inv[i] < 0) {
-                inv[i] = nx;
-                perm[nx++] = i;
-            }
-    }
+    internal_bit_order(n, c->n_pad, bdeg, plan, perm, inv, getenv("QKD_BIT_ORDER"));
     // the per-bit arrays in that order (the split kernels' DeviceCode view)
     std::vector<int32_t> bit_chk_s(bit_chk.size(), -1);
     std::vector<uint8_t> bit_deg_s(n, 0);
@@ -315,7 +405,9 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         if (!qkdr::xoshiro_charpoly(P))
             return set_error(QKD_ERR_DEVICE, "xoshiro256 characteristic polynomial: unexpected degree");
         const uint32_t kl = kKgSplitLanes;
-        c->kg_cb = (uint32_t)((n + kl - 1) / kl);
+        // (a multiple of 32: a lane's chunk of Alice's bits is whole 32-bit
+        // words, written by that lane alone, keygen_split_kernel)
+        c->kg_cb = (uint32_t)(((n + kl - 1) / kl + 31) / 32 * 32);
         c->kg_cs = (uint32_t)((draws - (uint64_t)n + kl - 1) / kl);
         std::vector<uint64_t> jp2((size_t)2 * kl * 4);
         for (uint32_t l = 0; l < kl; ++l) {
@@ -568,6 +660,30 @@ qkd_status qkd_code_get_adjacency(const qkd_code* c, int32_t* check_ptr, int32_t
     if (check_idx) std::memcpy(check_idx, c->check_idx.data(), c->check_idx.size() * 4);
     if (bit_ptr) std::memcpy(bit_ptr, c->bit_ptr.data(), c->bit_ptr.size() * 4);
     if (bit_idx) std::memcpy(bit_idx, c->bit_idx.data(), c->bit_idx.size() * 4);
+    return QKD_OK;
+}
+
+qkd_status qkd_debug_bit_order(int32_t n, int32_t m, const int32_t* cptr, const int32_t* cidx, const char* mode,
+                               int32_t* perm_out, uint32_t* plan_out, int32_t* n_tasks_out) {
+    clear_error();
+    if (n <= 0 || m <= 0 || !cptr || !cidx || !n_tasks_out) return set_error(QKD_ERR_INVALID_ARG, "bad arguments");
+    std::vector<int32_t> bdeg(n, 0), fill(n, 0), krow(cptr[m]);
+    for (int32_t j = 0; j < m; ++j)
+        for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) {
+            if (cidx[k] < 0 || cidx[k] >= n) return set_error(QKD_ERR_BAD_CODE, "bit index out of range");
+            bdeg[cidx[k]]++;
+        }
+    for (int32_t j = 0; j < m; ++j)
+        for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) krow[k] = fill[cidx[k]]++;
+    qkdp::WavePlan plan;
+    if (!qkdp::build_wave_plan(n, m, cptr, cidx, krow.data(), plan))
+        return set_error(QKD_ERR_UNSUPPORTED, "check degree outside [1, %d]", qkdp::kPlanMaxDegree);
+    const int32_t n_pad = round_up(n + 1, 64);
+    std::vector<int32_t> perm(n), inv(n, -1);
+    internal_bit_order(n, n_pad, bdeg, plan, perm, inv, mode);
+    if (perm_out) std::copy(perm.begin(), perm.end(), perm_out);
+    if (plan_out) std::copy(plan.word.begin(), plan.word.begin() + (size_t)plan.n_tasks * 64, plan_out);
+    *n_tasks_out = plan.n_tasks;
     return QKD_OK;
 }
 

@@ -56,13 +56,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));   // [lo, hi]; packed bina
 // The two series of phi_core, for a binary32 value or a packed pair (every
 // operation elementwise, so a pair's halves are bit for bit the scalar
 // results), in Horner's form:
-//   series_t(x) ~ (1 - e^-x) / x            (w = 1 - e^-x = x t, x < 0.35)
 //   series_h(s) ~ atanh(sqrt s) / sqrt s    (2 atanh(u) = 2u h, s = u^2 <= e^-2)
+//   series_g(y), below
 // Degree-4 near-minimax fits with binary32 coefficients
-// (tools/phi_poly_fit.py): at most 5.6e-8 / 7.2e-8 relative error including
-// the binary32 Horner evaluation, below the Taylor degree-6 forms they replaced
-// (6.0e-8 / 1.2e-7) with two operations fewer each; 2^-20 (kPhiRel) bounds
-// the whole evaluation, certified over every binary32 input on the GPU
+// (tools/phi_poly_fit.py): series_h at most 7.2e-8 relative error including
+// the binary32 Horner evaluation, below the Taylor degree-6 form it replaced
+// (1.2e-7) with two operations fewer; 2^-20 (kPhiRel) bounds the whole
+// evaluation, certified over every binary32 input on the GPU
 // (tests/test_spec.py::test_phi_bounds_exhaustive).
 // (Estrin's scheme, depth 2 for one more operation each, measured slower per
 // config-2 batch at degree 6: DESIGN.md §4.3.)
@@ -73,38 +73,43 @@ __device__ __forceinline__ V poly4(V z, float c0, float c1, float c2, float c3, 
     p = __builtin_elementwise_fma(z, p, V(c1));
     return __builtin_elementwise_fma(z, p, V(c0));
 }
+// g(y) = -ln(tanh(t) / t), t = sqrt(y) / 2: phi(x) = ln 2 - ln x + g(x^2)
+// for x < 1 (y < 1; g(0) = 0, g < 0.081), degree 4 without a constant term,
+// 1.3e-8 absolute at most with binary32 Horner evaluation (tools/phi_poly_fit.py)
 template <typename V>
-__device__ __forceinline__ V series_t(V x) {
-    return poly4(x, 1.0f, -0x1.ffffa6p-2f, 0x1.554208p-3f, -0x1.52ba68p-5f, 0x1.d9f3c2p-8f);
+__device__ __forceinline__ V series_g(V y) {
+    V p = __builtin_elementwise_fma(y, V(-0x1.6bf16ap-16f), V(0x1.627b52p-12f));
+    p = __builtin_elementwise_fma(y, p, V(-0x1.3e8026p-8f));
+    p = __builtin_elementwise_fma(y, p, V(0x1.555536p-4f));
+    return y * p;
 }
 template <typename V>
 __device__ __forceinline__ V series_h(V s) {
     return poly4(s, 1.0f, 0x1.55549p-2f, 0x1.9a05a2p-3f, 0x1.1b7792p-3f, 0x1.2e9afep-3f);
 }
-// phi (PSI: phi / ln 2) and an upper bound of |phi'(x)| = 1 / sinh(x)
-// (within a factor 2) at 0 < x <= kPhiHuge from u = e^-x (accurate) and x
-// (for the small-x series and the branch only).
+// phi's constant below x = 1 for a log taken of x / ln 2 (a psi-unit sum):
+// phi = ln 2 - ln x + g = (ln 2 - ln ln 2) - ln 2 log2(x / ln 2) + g
+constexpr float kPhiK = 1.05966010f;
+
+// phi (PSI: phi / ln 2) and an upper bound of |phi'(x)| = 1 / sinh(x) at
+// 0 < x <= kPhiHuge from u = e^-x (accurate), x (for g, the slope and the
+// branch) and lg = log2 of the log's argument: of x itself (LGP false) or of
+// P = x / ln 2, the psi-unit sum the output bound starts from (LGP true; x is
+// then the rounded P ln 2, which only feeds g, the slope and the branch).
 struct PhiVal {
     float v;
     float slope;
 };
 
-template <bool PSI>
-__device__ __forceinline__ PhiVal phi_core(float x, float u) {
-    // w = 1 - u: direct for x >= 0.35 (u <= 0.705: the subtraction costs under
-    // a bit), below it x series_t(x) (5.6e-8 relative at most)
-    // (series_t starts on x before u = e^-x is ready; the two series in one
-    // packed evaluation, which waits for u, measured no faster)
-    const float t = series_t(x);
-    const float w = x < 0.35f ? x * t : 1.0f - u;
-    const float w2 = 2.0f - w;
-    const float rw = __builtin_amdgcn_rcpf(w);
-    // x < 1: phi = ln((2 - w) / w) = ln 2 log2((2 - w) * rcp(w)); the
-    // argument is >= 2.16 (v_log_f32 is accurate to ~2^-22 absolute near 1,
-    // so the log is kept away from small results; rcp and the product add
-    // 1.5 ulp of the argument)
-    const float lg = __builtin_amdgcn_logf(w2 * rw);
-    const float vlo = PSI ? lg : kLn2 * lg;
+template <bool PSI, bool LGP>
+__device__ __forceinline__ PhiVal phi_core(float x, float u, float lg) {
+    static_assert(PSI != LGP, "psi values of a natural argument, or phi values of a psi-unit one");
+    // x < 1: phi = ln 2 - ln x + g(x^2) (psi: 1 - log2 x + g / ln 2): one
+    // log of the argument itself, off the polynomial's path (v_log_f32 is
+    // accurate to ~2^-22 absolute near 1, under a quarter of kPhiRel there)
+    const float g = series_g(x * x);
+    const float t = __builtin_fmaf(PSI ? -1.0f : -kLn2, lg, PSI ? 1.0f : kPhiK);
+    const float vlo = __builtin_fmaf(g, PSI ? kInvLn2 : 1.0f, t);
     // x >= 1: phi = 2 atanh(u) = 2u series_h(s), s = u^2 <= e^-2 (7.2e-8
     // relative at most, under 8 % of kPhiRel)
     const float s = u * u;
@@ -112,9 +117,10 @@ __device__ __forceinline__ PhiVal phi_core(float x, float u) {
     const float vhi = (u * (PSI ? 2.0f * kInvLn2 : 2.0f)) * h;
     PhiVal o;
     o.v = x < 1.0f ? vlo : vhi;
-    // |phi'(x)| = 1 / sinh(x) = 2u / (w (2 - w)) <= 2u / w (2 - w >= 1): an
-    // upper bound within a factor 2, which is all the tangents below need
-    o.slope = (2.0f * u) * rw;
+    // |phi'(x)| = 1 / sinh(x): below x = 1 at most 1 / x (sinh x > x), from x
+    // = 1 on 2u / (1 - u^2) <= 2u / (1 - e^-2) < 2.32 u (tangents need an
+    // upper bound only)
+    o.slope = x < 1.0f ? __builtin_amdgcn_rcpf(x) : 2.32f * u;
     return o;
 }
 
@@ -137,7 +143,7 @@ __device__ __forceinline__ float exp_neg(float x) {
 // bounds phi(a) above, and the tangent at a' stays below phi on [a', b].
 __device__ __forceinline__ f2 phi_bounds(float a, float b) {
     const float a1 = __builtin_amdgcn_fmed3f(a, 0.0f, kPhiHuge);     // min(a, kPhiHuge), a > 0
-    const PhiVal e = phi_core<true>(a1, exp_neg(a1));
+    const PhiVal e = phi_core<true, false>(a1, exp_neg(a1), __builtin_amdgcn_logf(a1));
     const float hi = __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f;
     const float t = __builtin_fmaf(-e.slope * ((1.0f + 2.0f * kPhiRel) * kInvLn2), b - a1, e.v * (1.0f - kPhiRel));
     return f2{t > 0.0f ? t : 0.0f, hi};     // lo: also for b = inf (t = -inf) and NaN
@@ -152,11 +158,12 @@ __device__ __forceinline__ void phi_bounds(float a, float b, float& lo, float& h
 // <= P_hi: at P_lo = 0 (the widened sum reached zero) the maximum is +inf and
 // the minimum is taken at P_hi; otherwise one evaluation at P_lo and its
 // tangent (both clamped to kPsiHuge as in phi_bounds). u = 2^-P needs no
-// argument split; x = P ln 2 (rounded) only steers the series and branch.
+// argument split, the log is taken of P itself; x = P ln 2 (rounded) only
+// feeds g, the slope and the branch.
 __device__ __forceinline__ f2 phi_bounds_out(float s_lo, float s_hi) {
     const bool zero = !(s_lo > 0.0f);
     const float at = __builtin_fminf(zero ? s_hi : s_lo, kPsiHuge);
-    const PhiVal e = phi_core<false>(at * kLn2, __builtin_amdgcn_exp2f(-at));
+    const PhiVal e = phi_core<false, true>(at * kLn2, __builtin_amdgcn_exp2f(-at), __builtin_amdgcn_logf(at));
     const float vmax = __builtin_fmaf(e.v, kPhiRel, e.v) + 1.0e-37f;
     const float tan = __builtin_fmaf(-e.slope * ((1.0f + 2.0f * kPhiRel) * kLn2), s_hi - at, e.v * (1.0f - kPhiRel));
     return f2{tan > 0.0f ? tan : 0.0f, zero ? __builtin_inff() : vmax};
@@ -167,30 +174,27 @@ __device__ __forceinline__ void phi_bounds_out(float s_lo, float s_hi, float& lo
     hi = r.y;
 }
 
-// phi_core twice, in the two halves of the packed binary32 unit: half 0 in
-// psi units (phi_core<true>), half 1 in phi units (phi_core<false>); every
-// operation is phi_core's, so each half is bit for bit its result.
+// phi_core twice, in the two halves of the packed binary32 unit: half 0
+// phi_core<true, false> (psi values of a natural argument), half 1
+// phi_core<false, true> (phi values of a psi-unit one), or, PSI1, both
+// phi_core<true, false>; every operation is phi_core's, so each half is bit
+// for bit its result.
 struct PhiVal2 {
     f2 v;
     f2 slope;
 };
-template <bool PSI1 = false>   // half 1 in psi units too
-__device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u) {
-    const f2 t = series_t(x);
-    const f2 ws = x * t;
-    const f2 wd = f2(1.0f) - u;
-    const f2 w = f2{x.x < 0.35f ? ws.x : wd.x, x.y < 0.35f ? ws.y : wd.y};
-    const f2 w2 = f2(2.0f) - w;
-    const f2 rw = f2{__builtin_amdgcn_rcpf(w.x), __builtin_amdgcn_rcpf(w.y)};
-    const f2 arg = w2 * rw;
-    const float lg1 = __builtin_amdgcn_logf(arg.y);
-    const f2 vlo = f2{__builtin_amdgcn_logf(arg.x), PSI1 ? lg1 : kLn2 * lg1};
+template <bool PSI1 = false>   // half 1 in psi units of a natural argument too
+__device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u, f2 lg) {
+    const f2 g = series_g(x * x);
+    const f2 t = __builtin_elementwise_fma(f2{-1.0f, PSI1 ? -1.0f : -kLn2}, lg, f2{1.0f, PSI1 ? 1.0f : kPhiK});
+    const f2 vlo = __builtin_elementwise_fma(g, f2{kInvLn2, PSI1 ? kInvLn2 : 1.0f}, t);
     const f2 s = u * u;
     const f2 h = series_h(s);
     const f2 vhi = (u * f2{2.0f * kInvLn2, PSI1 ? 2.0f * kInvLn2 : 2.0f}) * h;
+    const f2 sh = f2(2.32f) * u;
     PhiVal2 o;
     o.v = f2{x.x < 1.0f ? vlo.x : vhi.x, x.y < 1.0f ? vlo.y : vhi.y};
-    o.slope = (f2(2.0f) * u) * rw;
+    o.slope = f2{x.x < 1.0f ? __builtin_amdgcn_rcpf(x.x) : sh.x, x.y < 1.0f ? __builtin_amdgcn_rcpf(x.y) : sh.y};
     return o;
 }
 
@@ -215,7 +219,7 @@ __device__ __forceinline__ void phi_pair(float a, float b, float s_lo, float s_h
     const float rl = __builtin_fmaf(__builtin_fmaf(a1, L, -p0), kLn2, a1 * (L_lo * kLn2));
     const f2 e2 = f2{__builtin_amdgcn_exp2f(-p0), __builtin_amdgcn_exp2f(-P)};
     const f2 u = f2{__builtin_fmaf(e2.x, -rl, e2.x), e2.y};
-    const PhiVal2 e = phi_core_pair(f2{a1, P * kLn2}, u);
+    const PhiVal2 e = phi_core_pair(f2{a1, P * kLn2}, u, f2{__builtin_amdgcn_logf(a1), __builtin_amdgcn_logf(P)});
     const f2 v = e.v, slope = e.slope;
     // the bounds: phi(a) widened up; the tangent at the evaluation point, down
     const f2 hi = __builtin_elementwise_fma(v, f2(kPhiRel), v) + f2(1.0e-37f);
@@ -269,7 +273,7 @@ __device__ __forceinline__ void psi_of_exact2(double b0, double b1, f2& r0, f2& 
     const f2 rl = __builtin_elementwise_fma(__builtin_elementwise_fma(x, f2(L), -p), f2(kLn2), x * f2(L_lo * kLn2));
     const f2 e2 = f2{__builtin_amdgcn_exp2f(-p.x), __builtin_amdgcn_exp2f(-p.y)};
     const f2 u = __builtin_elementwise_fma(e2, -rl, e2);
-    const PhiVal2 e = phi_core_pair<true>(x, u);
+    const PhiVal2 e = phi_core_pair<true>(x, u, f2{__builtin_amdgcn_logf(x.x), __builtin_amdgcn_logf(x.y)});
     const f2 hi = __builtin_elementwise_fma(e.v, f2(kPhiRel), e.v) + f2(1.0e-37f);
     const f2 t = __builtin_elementwise_fma(-e.slope * f2((1.0f + 2.0f * kPhiRel) * kInvLn2), f2{a0.y, a1.y} - x,
                                            e.v * f2(1.0f - kPhiRel));
