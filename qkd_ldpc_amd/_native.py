@@ -135,7 +135,10 @@ def lib():
                                            P, P, P, P, P, P]),
             "qkd_trace_decode": (st, [P, P, P, U32, D, U32, P, P, P, P]),
         }
+        diagnostic = os.environ.get("QKD_AMD_LIB") and os.environ.get("QKD_AMD_DIAGNOSTIC") == "1"
         for name, (res, args) in sig.items():
+            if diagnostic and not hasattr(L, name):
+                continue          # an older build in an A/B run may lack newer debug entries
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -1558,6 +1558,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                              ? c->n_pat * kFoldTabPat : 0;
         // (QKD_FOLD_TABLE=0: the per-bit form; tests compare the two)
         if (const char* e = getenv("QKD_FOLD_TABLE")) if (atoi(e) == 0) a.ftab_entries = 0;
+        if (const char* e = getenv("QKD_SPEC_POLICY")) a.spec_always = strcmp(e, "always") == 0 ? 1u : 0u;
         const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, a.ftab_entries, esz,
                          budget);
         // (the binary32 rule's kernel keeps every slot in LDS: SplitStore<float, true>)

@@ -1412,7 +1412,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             ctl[1] = next_f;
             // speculate on the next frame unless a sixth of the frames
             // started so far (past the first 64) were replayed (kSpecReplayMax)
-            ctl[6] = launch_replays * 6u <= next_f + 64u ? 1u : 0u;
+            ctl[6] = (a.spec_always || launch_replays * 6u <= next_f + 64u) ? 1u : 0u;
         }
         __syncthreads();
     }

@@ -125,6 +125,9 @@ struct DecodeArgs {
     // frames replayed exactly in this launch (zeroed per launch): once they
     // pass a quarter of the frames started, later frames skip the speculation
     uint32_t* replay_count;
+    // QKD_SPEC_POLICY=always (tests): the in-launch replay policy never turns
+    // the speculation off, so the replay count depends on the frames alone
+    uint32_t spec_always;
     // checkpointed speculation (SPEC 2, high QBER): once an exact iteration
     // leaves at most ckpt_unsat checks unsatisfied, the messages are saved to
     // ckpt (ckpt_stride elements per workgroup) and the iterations continue on
