@@ -268,7 +268,7 @@ def measure_end_to_end(args, H, ws, seeds, F, Q, steps):
                              float(res.exact_qber[0].item()))
     return {"value": F * N_BITS * steps / el, "unit": "bit/s", "ms_per_step": el * 1e3 / steps,
             "steps": steps, "fer": st["fer"], "sum_iterations": st["sum_iters_sp"],
-            "what": "qkd_trials_batch: keygen_fast_kernel + frame_syn + decoder + key_match + counters"}
+            "what": "qkd_trials_batch: keygen_split_kernel + frame_syn + decoder (key compare in its epilogue) + counters"}
 
 
 def config3_sweep(args, H, Q, dev):

@@ -879,6 +879,35 @@ __global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_
     }
 }
 
+// The error positions without replaying the shuffle (keygen_split_kernel).
+// Step s of the forward shuffle (introduce_errors, qkd_ldpc_algorithm.cpp)
+// swaps a[s] with a[x_s], x_s <= s, and a[s] is still s when it does (earlier
+// steps touch only lower indices), so afterwards a[x_s] = s. Hence a[q]
+// (q < ne) is the last step s with x_s = q (last[q], an LDS atomicMax over
+// all steps) when there is one; otherwise the last step to touch q is step q
+// itself, which left there the value position x_q held just before it: the
+// last step s in [x_q, q) with x_s = x_q, or failing that (recursively) the
+// value x_q received from its own step. Position 0 is no step's index (its
+// value is 0 until a step writes it). Such positions (no later writer) are
+// ~q/N of them, ~2 per config-2 frame: the whole wave resolves each in turn,
+// scanning 64 steps per ballot. Every argument is wave-uniform.
+template <class XS>
+__device__ __forceinline__ uint32_t kg_resolve_wave(uint32_t q, const XS& xs, uint32_t lane) {
+    uint32_t t = q, p = xs(q);
+    for (;;) {
+        const int lo = p > 1u ? (int)p : 1;
+        for (int base = (int)t - 1; base >= lo; base -= 64) {
+            const int st = base - (int)lane;
+            const bool hit = st >= lo && xs((uint32_t)st) == p;
+            const uint64_t hb = __ballot(hit);
+            if (hb) return (uint32_t)(base - (__ffsll((unsigned long long)hb) - 1));
+        }
+        if (p == 0) return 0;
+        t = p;
+        p = xs(p);
+    }
+}
+
 // The same key pair by two waves per workgroup (the default generator): in the
 // one-wave form every lane's chunk mixes Alice's bits and shuffle draws, so
 // the wave runs both loop bodies on every draw. Here wave 0 draws only Alice's
@@ -887,11 +916,13 @@ __global__ __launch_bounds__(kKeygenBlock) void keygen_fast_kernel(const uint64_
 // (lane l: from draw N + l * cs): each lane jumps once (its own polynomial,
 // c->d_jpoly2), every loop is uniform. A frame takes kKgSplitLanes lanes of
 // each wave, so a workgroup holds kKgSplitFrames frames: fewer lanes per
-// frame mean longer chunks but fewer 256-step jumps per frame. The shuffle's
-// low steps are replayed and the last writers found exactly as in
-// keygen_fast_kernel; the flips land in an LDS copy of the key, and both keys
+// frame mean longer chunks but fewer 256-step jumps per frame. Every step's
+// swap partner below ne goes into last[] (LDS atomicMax), the low steps'
+// partners also into park[]; the error positions then follow without a serial
+// replay (kg_resolve). The flips land in an LDS copy of the key, and both keys
 // leave as whole coalesced words.
-// LDS per frame: low[ne], last[ne], park[ne / 2 + 1], alice[words], bob[words].
+// LDS per frame: low[ne] (the serial path's), last[ne], park[ne / 2 + 1],
+// alice[words], bob[words].
 template <bool R32>
 __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
                                                            uint32_t words, uint32_t ne, uint32_t cb, uint32_t cs,
@@ -932,10 +963,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
     for (uint32_t sl = 0; sl < FPW; ++sl) {
         uint32_t* lo = reinterpret_cast<uint32_t*>(frame_lds(sl));
         uint64_t* a = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(lo + 2 * ne) + ne / 2 + 1);
-        for (uint32_t q = tid; q < ne; q += 128) {
-            lo[q] = q;
-            lo[ne + q] = 0;
-        }
+        for (uint32_t q = tid; q < ne; q += 128) lo[ne + q] = 0;
         for (uint32_t w = tid; w < words; w += 128) a[w] = 0;
     }
     if (tid < FPW) {
@@ -980,7 +1008,9 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         uint64_t d = (uint64_t)n + (uint64_t)l * cs;
         const uint64_t end = live ? min(d + cs, draws) : d;
         if (d < end && d < pair0) {                      // the lone draw (even N): lane 0
-            s_lone[slot] = (uint32_t)(g.next_fast() >> 63);
+            const uint32_t x = (uint32_t)(g.next_fast() >> 63);
+            s_lone[slot] = x;
+            if (x < ne) atomicMax(&last[x], 1u);
             ++d;
         }
         uint32_t i = i0 + 2u * (uint32_t)(d - pair0);
@@ -1002,12 +1032,9 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
             const bool lo = r0 < 0, hi = r0 >= (int32_t)bb;
             const uint32_t q = q0 + (hi ? 1u : 0u) - (lo ? 1u : 0u);
             const int32_t rem = r0 + (lo ? (int32_t)bb : 0) - (hi ? (int32_t)bb : 0);
-            if (i < ne) {
-                park[(i - i0) >> 1] = make_uint2(q, (uint32_t)rem);
-            } else {
-                if (q < ne) atomicMax(&last[q], i);
-                if ((uint32_t)rem < ne) atomicMax(&last[rem], i + 1);
-            }
+            if (i < ne) park[(i - i0) >> 1] = make_uint2(q, (uint32_t)rem);
+            if (q < ne) atomicMax(&last[q], i);
+            if ((uint32_t)rem < ne) atomicMax(&last[rem], i + 1);
             rg += 4u * i + 10u;                          // (i + 3)(i + 4)
             i += 2u;
         }
@@ -1017,7 +1044,9 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         for (uint64_t d = first; d < end; ++d) {
             const uint64_t r = g.next();
             if (d < pair0) {
-                s_lone[slot] = (uint32_t)(r >> 63);
+                const uint32_t x = (uint32_t)(r >> 63);
+                s_lone[slot] = x;
+                if (x < ne) atomicMax(&last[x], 1u);
                 continue;
             }
             const uint32_t i = i0 + 2u * (uint32_t)(d - pair0);
@@ -1034,12 +1063,9 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
                 qa = (uint32_t)a;
                 qb = (uint32_t)(x - a * b1);
             }
-            if (i < ne) {
-                park[(i - i0) >> 1] = make_uint2(qa, qb);
-            } else {
-                if (qa < ne) atomicMax(&last[qa], i);
-                if (qb < ne) atomicMax(&last[qb], i + 1);
-            }
+            if (i < ne) park[(i - i0) >> 1] = make_uint2(qa, qb);
+            if (qa < ne) atomicMax(&last[qa], i);
+            if (qb < ne) atomicMax(&last[qb], i + 1);
         }
     }
     __syncthreads();
@@ -1062,27 +1088,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         for (uint32_t q = 0; q < ne; ++q) B[low[q] >> 6] ^= 1ull << (low[q] & 63);
         if (exact_q) exact_q[f] = (double)ne / (double)n;
     }
-    if (live && !rej && shuffle_wave && l == 0) {
-        // replay of the steps with index < ne (shuffle_low_positions' step())
-        auto step = [&](uint32_t si, uint32_t x) {
-            if (si < ne) {
-                const uint32_t v = low[x];
-                low[x] = si;
-                low[si] = v;
-            } else if (x < ne) {
-                low[x] = si;
-            }
-        };
-        if (n > 1) {
-            if (even) step(1, s_lone[slot]);
-            for (uint32_t i = i0; i < ne && i < n; i += 2) {
-                const uint2 q = park[(i - i0) >> 1];
-                step(i, q.x);
-                step(i + 1, q.y);
-            }
-        }
-        if (exact_q) exact_q[f] = (double)ne / (double)n;
-    }
+    if (live && !rej && shuffle_wave && l == 0 && exact_q) exact_q[f] = (double)ne / (double)n;
     // (the rest per frame slot, all 128 threads; a rejected frame is done)
     for (uint32_t sl = 0; sl < FPW; ++sl) {
         uint64_t* a = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(
@@ -1094,10 +1100,25 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         const uint32_t fs = blockIdx.x * FPW + sl;
         if (fs >= n_frames || s_reject[sl]) continue;                // (workgroup-uniform)
         uint32_t* lo = reinterpret_cast<uint32_t*>(frame_lds(sl));
+        const uint2* pk = reinterpret_cast<const uint2*>(lo + 2 * ne);
         uint64_t* b = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(lo + 2 * ne) + ne / 2 + 1) + words;
-        for (uint32_t q = tid; q < ne; q += 128) {
-            const uint32_t pos = lo[ne + q] ? lo[ne + q] : lo[q];
-            atomicXor(reinterpret_cast<unsigned long long*>(&b[pos >> 6]), 1ull << (pos & 63u));
+        // x_s: the position step s (1 <= s < ne) swaps with
+        auto xs = [&](uint32_t st) -> uint32_t {
+            if (even && st == 1) return s_lone[sl];
+            const uint2 pr = pk[(st - i0) >> 1];
+            return ((st - i0) & 1u) ? pr.y : pr.x;
+        };
+        for (uint32_t q0 = 0; q0 < ne; q0 += 128) {            // (uniform trip count: the scans use every lane)
+            const uint32_t q = q0 + tid;
+            uint32_t pos = q < ne ? lo[ne + q] : 1u;
+            uint64_t rare = __ballot(pos == 0 && q > 0);
+            while (rare) {
+                const uint32_t src = (uint32_t)(__ffsll((unsigned long long)rare) - 1);
+                rare &= rare - 1;
+                const uint32_t r = kg_resolve_wave(q0 + (tid & ~63u) + src, xs, lane);
+                if (lane == src) pos = r;
+            }
+            if (q < ne) atomicXor(reinterpret_cast<unsigned long long*>(&b[pos >> 6]), 1ull << (pos & 63u));
         }
     }
     __syncthreads();

@@ -34,12 +34,12 @@ if [ -n "${PMC:-}" ]; then
     env $(libenv $l) QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=$(libpath $l) timeout -s KILL 120 rocprofv3 --pmc $PMC --output-format csv \
       -d $O/pmc_$l -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-e2e \
       --no-sweeps > $O/pmc_$l.log 2>&1 || { echo "pmc $l failed"; tail $O/pmc_$l.log; exit 1; }
-    python3 - $O/pmc_$l $l <<'PY'
+    python3 - $O/pmc_$l $l ${PMC_KERNEL:-decode} <<'PY'
 import csv, glob, sys, collections
 v = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "decode" in r["Kernel_Name"]:
+        if sys.argv[3] in r["Kernel_Name"]:
             v[r["Counter_Name"]].append(float(r["Counter_Value"]))
 print(sys.argv[2], {k: round(sum(x) / len(x)) for k, x in v.items()})
 PY
