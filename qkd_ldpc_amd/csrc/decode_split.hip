@@ -1549,8 +1549,140 @@ __global__ void zout_unpack_kernel(const uint64_t* zout, const int32_t* inv, uin
     out[gid] = (uint8_t)((zout[f * words + (q >> 6)] >> (q & 63)) & 1u);
 }
 
+// frame_syn_kernel's work bit-sliced over frames: a workgroup takes 16
+// frames and first transposes their keys into 32-bit slices T[i] (bit f =
+// Alice's bit i of frame f, bit 16 + f = Bob's; one ballot gives two bit
+// positions: lanes 0-31 hold word w of the 16 frames' two keys, lanes 32-63
+// word w + 1). A check's parities for all 16 frames and both keys are then
+// one XOR of its row's slices, and each internal-order key word one slice read
+// per lane followed by a ballot per frame and key. Per frame this reads LDS
+// ~15x less than frame_syn_kernel (an 8-byte read per row entry and frame).
+// LDS: words * 64 slices of 4 bytes (N <= 40960 in 160 KB).
+constexpr int kSlicedFrames = 16;
+constexpr int kSlicedBlock = 1024;
+constexpr int kSlicedPre = 8;        // key-word pairs a wave loads ahead
+// lane `at` (wave-uniform) of x takes the wave-uniform value m
+__device__ __forceinline__ uint64_t put_lane(uint64_t x, uint32_t at, uint64_t m) {
+    return (threadIdx.x & 63u) == at ? m : x;
+}
+__global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCode c, uint64_t* alice_w,
+                                                                        uint64_t* bob_w, uint32_t words,
+                                                                        uint32_t n_frames, uint32_t lsign,
+                                                                        uint32_t* synw, uint32_t* counter) {
+    extern __shared__ uint32_t T[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    constexpr uint32_t NW = kSlicedBlock / 64;
+    if (blockIdx.x == 0 && tid < 2) counter[tid] = 0;     // (the decoder's queue, as frame_syn_kernel)
+    const uint32_t f0 = blockIdx.x * kSlicedFrames;
+    const uint32_t nf = min((uint32_t)kSlicedFrames, n_frames - f0);
+    const uint32_t fr = lane & 15u;
+    const bool bob_lane = (lane & 16u) != 0;
+    const uint32_t half = lane >> 5;                      // which word of the pair
+    const uint32_t pairs = (words + 1) / 2;
+    // 1. slices: wave takes word pairs p = wave, wave + NW, ..., loading up to
+    //    kSlicedPre of them ahead; lane b keeps the ballot of bit b: the
+    //    slices of positions 64 (2p) + b (low half) and 64 (2p + 1) + b (high)
+    auto load_pair = [&](uint32_t p) -> uint64_t {
+        const uint32_t w = 2 * p + half;
+        if (p >= pairs || w >= words || fr >= nf) return 0;
+        return (bob_lane ? bob_w : alice_w)[(size_t)(f0 + fr) * words + w];
+    };
+    auto slice_pair = [&](uint32_t p, uint64_t v) {
+        // (four independent select chains: each lane takes exactly one value)
+        uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+        const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
+#pragma unroll
+        for (uint32_t b = 0; b < 32; b += 2) {
+            m0 = put_lane(m0, b, __ballot((vlo >> b) & 1u));
+            m1 = put_lane(m1, b + 1, __ballot((vlo >> (b + 1)) & 1u));
+            m2 = put_lane(m2, 32 + b, __ballot((vhi >> b) & 1u));
+            m3 = put_lane(m3, 33 + b, __ballot((vhi >> (b + 1)) & 1u));
+        }
+        const uint64_t mine = m0 | m1 | m2 | m3;
+        T[(size_t)(2 * p) * 64 + lane] = (uint32_t)mine;
+        if (2 * p + 1 < words) T[(size_t)(2 * p + 1) * 64 + lane] = (uint32_t)(mine >> 32);
+    };
+    for (uint32_t p0 = wave; p0 < pairs; p0 += NW * kSlicedPre) {
+        uint64_t v[kSlicedPre];
+#pragma unroll
+        for (int k = 0; k < kSlicedPre; ++k) v[k] = load_pair(p0 + (uint32_t)k * NW);
+#pragma unroll
+        for (int k = 0; k < kSlicedPre; ++k)
+            if (p0 + (uint32_t)k * NW < pairs) slice_pair(p0 + (uint32_t)k * NW, v[k]);
+    }
+    __syncthreads();
+    // 2. syndromes: lane = check; 64 checks per wave and pass, then per frame
+    //    two ballots (target s_j, first-product sign q_j) that lane f keeps
+    const int m_words = decode_m_words(c.m);
+    const int rs = c.chk_rs;
+    for (uint32_t j0 = wave * 64; j0 < (uint32_t)c.m; j0 += kSlicedBlock) {
+        const uint32_t j = j0 + lane;
+        uint32_t P = 0, deg = 0;
+        if (j < (uint32_t)c.m) {
+            const uint16_t* row = c.chk_rows16 + (size_t)j * rs;
+            for (int h = 0; h < rs; h += 8) {
+                const uint4 r = *reinterpret_cast<const uint4*>(row + h);
+                const uint32_t e[8] = {r.x & 0xffffu, r.x >> 16, r.y & 0xffffu, r.y >> 16,
+                                       r.z & 0xffffu, r.z >> 16, r.w & 0xffffu, r.w >> 16};
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (e[k] != 0xffffu) {
+                        P ^= T[e[k]];
+                        deg++;
+                    }
+            }
+        }
+        const uint32_t Q = P ^ (P >> 16) ^ ((lsign & deg) ? 0xffffu : 0u);   // low 16: q bits
+        uint64_t sk = 0, qk = 0;
+        for (uint32_t f = 0; f < nf; ++f) {
+            sk = put_lane(sk, f, __ballot((P >> f) & 1u));
+            qk = put_lane(qk, f, __ballot((Q >> f) & 1u));
+        }
+        if (lane < nf) {
+            uint32_t* o = synw + (size_t)(f0 + lane) * 2 * m_words;
+            o[j0 >> 5] = (uint32_t)sk;
+            o[(j0 >> 5) + 1] = (uint32_t)(sk >> 32);
+            o[m_words + (j0 >> 5)] = (uint32_t)qk;
+            o[m_words + (j0 >> 5) + 1] = (uint32_t)(qk >> 32);
+        }
+    }
+    // 3. the keys in the internal order (DeviceCode::perm), in place: word w's
+    //    lane l reads the slice of original bit perm[64 w + l]; per frame a
+    //    ballot per key, lane f keeping Alice's word of frame f, lane 32 + f Bob's
+    for (uint32_t w = wave; w < words; w += NW) {
+        const uint32_t q = w * 64 + lane;
+        const uint32_t S = q < (uint32_t)c.n ? T[c.perm[q]] : 0u;
+        uint64_t ma = 0, mb = 0;
+        for (uint32_t f = 0; f < nf; ++f) {
+            ma = put_lane(ma, f, __ballot((S >> f) & 1u));
+            mb = put_lane(mb, 32 + f, __ballot((S >> (16 + f)) & 1u));
+        }
+        const uint64_t mine = ma | mb;
+        const uint32_t g = lane & 31u;
+        if (g < nf) (lane < 32 ? alice_w : bob_w)[(size_t)(f0 + g) * words + w] = mine;
+    }
+}
+
 hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
+    // the bit-sliced form when its slices fit LDS and the compact rows exist
+    // (QKD_SYN_SLICED=0: frame_syn_kernel; tests compare the two)
+    const size_t slds = (size_t)a.words * 64 * sizeof(uint32_t);
+    const char* se = getenv("QKD_SYN_SLICED");
+    if (a.code.chk_rows16 && slds <= 160 * 1024 && !(se && atoi(se) == 0)) {
+        static bool attr = false;
+        if (!attr) {
+            const hipError_t e = hipFuncSetAttribute((const void*)frame_syn_sliced_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+        hipLaunchKernelGGL(frame_syn_sliced_kernel, dim3((a.n_frames + kSlicedFrames - 1) / kSlicedFrames),
+                           dim3(kSlicedBlock), slds, stream, a.code, const_cast<uint64_t*>(a.alice_w),
+                           const_cast<uint64_t*>(a.bob_w), a.words, a.n_frames, lsign,
+                           const_cast<uint32_t*>(a.synw), a.counter);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)kSynFrames * 2 * a.words * sizeof(uint64_t);
     hipLaunchKernelGGL(frame_syn_kernel, dim3((a.n_frames + kSynFrames - 1) / kSynFrames), dim3(kSynBlock), lds,
                        stream, a.code, const_cast<uint64_t*>(a.alice_w), const_cast<uint64_t*>(a.bob_w), a.words,

@@ -47,8 +47,10 @@ static void free_device(qkd_code* c) {
     c->d_bit_code = nullptr;
     if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
     for (void* p : {(void*)c->d_perm, (void*)c->d_inv, (void*)c->d_bit_chk_s, (void*)c->d_bit_deg_s,
-                    (void*)c->d_bit_pat_s})
+                    (void*)c->d_bit_pat_s, (void*)c->d_chk_rows16})
         if (p) (void)hipFree(p);
+    c->d_chk_rows16 = nullptr;
+    c->chk_rs = 0;
     c->d_perm = c->d_inv = c->d_bit_chk_s = nullptr;
     c->d_bit_deg_s = nullptr;
     c->d_bit_pat_s = nullptr;
@@ -338,6 +340,18 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     QKD_HIP(hipMemcpy(c->d_perm, perm.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice));
     QKD_HIP(hipMalloc(&c->d_inv, (size_t)n * sizeof(int32_t)));
     QKD_HIP(hipMemcpy(c->d_inv, inv.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice));
+    // frame_syn_sliced_kernel's check rows (N < 65535, check degree <= 16):
+    // each check's bits as one or two 16-byte rows of uint16 (0xffff past
+    // the row), one load per row
+    if (n < 65535 && max_dc <= 16) {
+        const int32_t rs = max_dc <= 8 ? 8 : 16;
+        std::vector<uint16_t> rows((size_t)m * rs, 0xffff);
+        for (int32_t j = 0; j < m; ++j)
+            for (int32_t k = 0; k < chk_deg[j]; ++k) rows[(size_t)j * rs + k] = (uint16_t)chk_bits[(size_t)k * c->m_pad + j];
+        QKD_HIP(hipMalloc(&c->d_chk_rows16, rows.size() * sizeof(uint16_t)));
+        QKD_HIP(hipMemcpy(c->d_chk_rows16, rows.data(), rows.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+        c->chk_rs = rs;
+    }
     QKD_HIP(hipMalloc(&c->d_bit_chk_s, bit_chk_s.size() * sizeof(int32_t)));
     QKD_HIP(hipMemcpy(c->d_bit_chk_s, bit_chk_s.data(), bit_chk_s.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     QKD_HIP(hipMalloc(&c->d_bit_deg_s, bit_deg_s.size()));

@@ -99,6 +99,11 @@ struct DeviceCode {
     // (original order). bit_code and plan_slot exist in the internal order only.
     const int32_t* perm;
     const int32_t* inv;
+    // frame_syn_sliced_kernel (split view, N < 65535, check degree <= 16;
+    // else nullptr): chk_rows16[j * chk_rs + k] = bit k of check j (0xffff
+    // past the row; chk_rs 8 or 16)
+    const uint16_t* chk_rows16;
+    int32_t chk_rs;
 };
 
 }  // namespace qkd
@@ -187,6 +192,9 @@ struct qkd_code {
     // per-bit arrays in it
     int32_t* d_perm = nullptr;
     int32_t* d_inv = nullptr;
+    // frame_syn_sliced_kernel's compact check rows (host.cpp)
+    uint16_t* d_chk_rows16 = nullptr;
+    int32_t chk_rs = 0;
     int32_t* d_bit_chk_s = nullptr;
     uint8_t* d_bit_deg_s = nullptr;
     uint16_t* d_bit_pat_s = nullptr;
@@ -210,13 +218,15 @@ struct qkd_code {
     qkd::DeviceCode view() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
-                               n_pat, d_bit_pat, d_pat_deg, nullptr, nullptr, nullptr, nullptr};
+                               n_pat, d_bit_pat, d_pat_deg, nullptr, nullptr, nullptr, nullptr,
+                               nullptr, 0};
     }
     // the split kernels' view (internal bit order, DeviceCode::perm)
     qkd::DeviceCode view_split() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk_s, nullptr, d_bit_deg_s,
-                               n_pat, d_bit_pat_s, d_pat_deg, d_bit_code, d_plan_slot, d_perm, d_inv};
+                               n_pat, d_bit_pat_s, d_pat_deg, d_bit_code, d_plan_slot, d_perm, d_inv,
+                               d_chk_rows16, chk_rs};
     }
 };
 

@@ -196,7 +196,11 @@ def test_decoded_qber_of_one_rejected(Q, H):
 
 # ---- fused trials: BASELINE configs 2 and 3 per frame ----------------------------------
 
-def test_trials_config2_full_batch(Q, H, probe, golden_vectors):
+@pytest.mark.parametrize("sliced", ["1", "0"])
+def test_trials_config2_full_batch(Q, H, probe, golden_vectors, monkeypatch, sliced):
+    """sliced 1: the frame syndromes and internal-order keys by
+    frame_syn_sliced_kernel (the default); 0: by frame_syn_kernel."""
+    monkeypatch.setenv("QKD_SYN_SLICED", sliced)
     seeds = Q.make_seeds(777, 4096)
     r = Q.run_trials(H, seeds_dev(seeds), 0.02, 0, 50, 100.0, True)
     torch.cuda.synchronize()

@@ -134,3 +134,27 @@ def test_large_code_variants_decode(Q, big_codes, variant):
     r = Q.run_trials(H, seeds, 0.02, 0, 40, variant=variant)
     torch.cuda.synchronize()
     assert r.syndromes_match.cpu().numpy().all() and r.keys_match.cpu().numpy().all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dv,dc", [(3, 6), (3, 12), (2, 16)])
+def test_frame_syn_sliced_equals_plain(monkeypatch, dv, dc):
+    """frame_syn_sliced_kernel (frames bit-sliced, uint16 check rows of width
+    8 or 16) against frame_syn_kernel (QKD_SYN_SLICED=0): the
+    same decoded words, iterations and flags on the keys path."""
+    import torch
+    import qkd_ldpc_amd as Q
+    n = 2400
+    m, cp, ci = regular_code(n, dv, dc, seed=dc)
+    H = Q.HMatrix.from_check_lists(n, cp, ci)
+    seeds = torch.from_numpy(Q.make_seeds(99, 600).view(np.int64)).cuda()
+    a, b, q = Q.keygen(H, seeds, 0.01)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("QKD_SYN_SLICED", mode)
+        r = Q.qkd_ldpc(H, a, b, float(q[0]), 50, 100.0, True, want_bits=True)
+        torch.cuda.synchronize()
+        out[mode] = r
+    x, y = out["1"], out["0"]
+    assert torch.equal(x.iterations, y.iterations) and torch.equal(x.bits, y.bits)
+    assert torch.equal(x.keys_match, y.keys_match) and torch.equal(x.syndromes_match, y.syndromes_match)
