@@ -964,7 +964,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         uint32_t* lo = reinterpret_cast<uint32_t*>(frame_lds(sl));
         uint64_t* a = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(lo + 2 * ne) + ne / 2 + 1);
         for (uint32_t q = tid; q < ne; q += 128) lo[ne + q] = 0;
-        for (uint32_t w = tid; w < words; w += 128) a[w] = 0;
+        for (uint32_t w = tid; w < 2 * words; w += 128) a[w] = 0;   // Alice's words, then the flip mask
     }
     if (tid < FPW) {
         s_lone[tid] = 0;
@@ -1089,13 +1089,8 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         if (exact_q) exact_q[f] = (double)ne / (double)n;
     }
     if (live && !rej && shuffle_wave && l == 0 && exact_q) exact_q[f] = (double)ne / (double)n;
-    // (the rest per frame slot, all 128 threads; a rejected frame is done)
-    for (uint32_t sl = 0; sl < FPW; ++sl) {
-        uint64_t* a = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(
-                          reinterpret_cast<uint32_t*>(frame_lds(sl)) + 2 * ne) + ne / 2 + 1);
-        for (uint32_t w = tid; w < words; w += 128) a[words + w] = a[w];
-    }
-    __syncthreads();
+    // (the rest per frame slot, all 128 threads; a rejected frame is done):
+    // the flips into a mask beside Alice's words, Bob's key = Alice's ^ mask
     for (uint32_t sl = 0; sl < FPW; ++sl) {
         const uint32_t fs = blockIdx.x * FPW + sl;
         if (fs >= n_frames || s_reject[sl]) continue;                // (workgroup-uniform)
@@ -1129,7 +1124,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
                                 reinterpret_cast<const uint32_t*>(frame_lds(sl)) + 2 * ne) + ne / 2 + 1);
         for (uint32_t w = tid; w < words; w += 128) {
             alice_w[(size_t)fs * words + w] = a[w];
-            bob_w[(size_t)fs * words + w] = a[words + w];
+            bob_w[(size_t)fs * words + w] = a[w] ^ a[words + w];
         }
     }
 }
