@@ -580,7 +580,7 @@ def main():
             "roofline": roofline_block(
                 args.variant, alg_bytes, avg_kernel_s, avg_call_s,
                 "decode_split_kernel (HIP events around its launch on its stream); call = "
-                "qkd_qkd_ldpc_batch: pack + frame_syn_kernel + decoder + key_match_kernel"),
+                "qkd_qkd_ldpc_batch: pack + frame syndromes + decoder (key compare in its epilogue)"),
             "speculation": {
                 "replayed_frames": replays,
                 "frames": F * (prewarm_steps + args.warmup + args.steps + 5 + (3 if args.kernel_events == "off" else 0)),
