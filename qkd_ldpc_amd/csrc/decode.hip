@@ -911,18 +911,18 @@ __device__ __forceinline__ uint32_t kg_resolve_wave(uint32_t q, const XS& xs, ui
 // The same key pair by two waves per workgroup (the default generator): in the
 // one-wave form every lane's chunk mixes Alice's bits and shuffle draws, so
 // the wave runs both loop bodies on every draw. Here wave 0 draws only Alice's
-// bits (a frame's lane l: draws [l * cb, (l + 1) * cb), OR-ed into LDS words,
-// as chunks need not end on word boundaries) and wave 1 only the shuffle's
+// bits (a frame's lane l: draws [l * cb, (l + 1) * cb), cb a multiple of 32,
+// written as whole 32-bit LDS words) and wave 1 only the shuffle's
 // (lane l: from draw N + l * cs): each lane jumps once (its own polynomial,
 // c->d_jpoly2), every loop is uniform. A frame takes kKgSplitLanes lanes of
 // each wave, so a workgroup holds kKgSplitFrames frames: fewer lanes per
 // frame mean longer chunks but fewer 256-step jumps per frame. Every step's
 // swap partner below ne goes into last[] (LDS atomicMax), the low steps'
 // partners also into park[]; the error positions then follow without a serial
-// replay (kg_resolve). The flips land in an LDS copy of the key, and both keys
-// leave as whole coalesced words.
+// replay (kg_resolve_wave). The flips land in a mask beside Alice's words,
+// and both keys leave as whole coalesced words (Bob's as Alice ^ mask).
 // LDS per frame: low[ne] (the serial path's), last[ne], park[ne / 2 + 1],
-// alice[words], bob[words].
+// alice[words], flips[words].
 template <bool R32>
 __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
                                                            uint32_t words, uint32_t ne, uint32_t cb, uint32_t cs,
