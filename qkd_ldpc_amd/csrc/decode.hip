@@ -924,7 +924,7 @@ __device__ __forceinline__ uint32_t kg_resolve_wave(uint32_t q, const XS& xs, ui
 // LDS per frame: low[ne] (the serial path's), last[ne], park[ne / 2 + 1],
 // alice[words], flips[words].
 template <bool R32>
-__global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
+__global__ __launch_bounds__(kKgBlock) void keygen_split_kernel(const uint64_t* seeds, uint64_t offset, uint32_t n,
                                                            uint32_t words, uint32_t ne, uint32_t cb, uint32_t cs,
                                                            uint32_t n_frames, const uint64_t* __restrict__ jpoly,
                                                            uint64_t* alice_w, uint64_t* bob_w, double* exact_q,
@@ -934,8 +934,11 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
     __shared__ uint32_t s_lone[FPW], s_reject[FPW];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
-    const bool shuffle_wave = tid >= 64;                        // wave-uniform
-    const uint32_t slot = lane / KL;                            // this lane's frame in the workgroup
+    // (the wave index through readfirstlane: the compiler then knows it, and a
+    // frame's seed, wave-uniform, so the jumps' state steps stay scalar)
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const bool shuffle_wave = (wv & 1u) != 0;
+    const uint32_t slot = (wv >> 1) * (64 / KL) + lane / KL;   // this lane's frame in the workgroup
     const uint32_t l = lane % KL;                               // and its lane in that frame
     // (per frame an even number of 32-bit words before the key words)
     const uint32_t frame_u64 = (2 * ne + 2 * (ne / 2 + 1)) / 2 + 2 * words;
@@ -963,8 +966,8 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
     for (uint32_t sl = 0; sl < FPW; ++sl) {
         uint32_t* lo = reinterpret_cast<uint32_t*>(frame_lds(sl));
         uint64_t* a = reinterpret_cast<uint64_t*>(reinterpret_cast<uint2*>(lo + 2 * ne) + ne / 2 + 1);
-        for (uint32_t q = tid; q < ne; q += 128) lo[ne + q] = 0;
-        for (uint32_t w = tid; w < 2 * words; w += 128) a[w] = 0;   // Alice's words, then the flip mask
+        for (uint32_t q = tid; q < ne; q += kKgBlock) lo[ne + q] = 0;
+        for (uint32_t w = tid; w < 2 * words; w += kKgBlock) a[w] = 0;   // Alice's words, then the flip mask
     }
     if (tid < FPW) {
         s_lone[tid] = 0;
@@ -1089,7 +1092,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         if (exact_q) exact_q[f] = (double)ne / (double)n;
     }
     if (live && !rej && shuffle_wave && l == 0 && exact_q) exact_q[f] = (double)ne / (double)n;
-    // (the rest per frame slot, all 128 threads; a rejected frame is done):
+    // (the rest per frame slot, all kKgBlock threads; a rejected frame is done):
     // the flips into a mask beside Alice's words, Bob's key = Alice's ^ mask
     for (uint32_t sl = 0; sl < FPW; ++sl) {
         const uint32_t fs = blockIdx.x * FPW + sl;
@@ -1103,7 +1106,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
             const uint2 pr = pk[(st - i0) >> 1];
             return ((st - i0) & 1u) ? pr.y : pr.x;
         };
-        for (uint32_t q0 = 0; q0 < ne; q0 += 128) {            // (uniform trip count: the scans use every lane)
+        for (uint32_t q0 = 0; q0 < ne; q0 += kKgBlock) {       // (uniform trip count: the scans use every lane)
             const uint32_t q = q0 + tid;
             uint32_t pos = q < ne ? lo[ne + q] : 1u;
             uint64_t rare = __ballot(pos == 0 && q > 0);
@@ -1122,7 +1125,7 @@ __global__ __launch_bounds__(128) void keygen_split_kernel(const uint64_t* seeds
         if (fs >= n_frames || s_reject[sl]) continue;
         const uint64_t* a = reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint2*>(
                                 reinterpret_cast<const uint32_t*>(frame_lds(sl)) + 2 * ne) + ne / 2 + 1);
-        for (uint32_t w = tid; w < words; w += 128) {
+        for (uint32_t w = tid; w < words; w += kKgBlock) {
             alice_w[(size_t)fs * words + w] = a[w];
             bob_w[(size_t)fs * words + w] = a[w] ^ a[words + w];
         }
@@ -1966,7 +1969,7 @@ static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uin
                                                   2 * (size_t)words * sizeof(uint64_t));
     if (ne <= kKeygenFastMaxErrors && c->d_jpoly2 && !serial && !matrix && !lanes && lds2 <= kLdsBytesMax) {
         auto* const kg = c->n <= 65536 ? keygen_split_kernel<true> : keygen_split_kernel<false>;
-        hipLaunchKernelGGL(kg, dim3((unsigned)((n_frames + kKgSplitFrames - 1) / kKgSplitFrames)), dim3(128), lds2,
+        hipLaunchKernelGGL(kg, dim3((unsigned)((n_frames + kKgSplitFrames - 1) / kKgSplitFrames)), dim3(kKgBlock), lds2,
                            stream, seeds, offset, (uint32_t)c->n, words, (uint32_t)ne, c->kg_cb, c->kg_cs,
                            (uint32_t)n_frames, c->d_jpoly2, ws->alice_w, ws->bob_w, exact_q, replay);
         QKD_HIP(hipGetLastError());

@@ -52,7 +52,13 @@ constexpr uint32_t kKeygenFastMaxErrors = 4096;
 #define QKD_KG_SPLIT_LANES 64
 #endif
 constexpr uint32_t kKgSplitLanes = QKD_KG_SPLIT_LANES;
-constexpr uint32_t kKgSplitFrames = 64 / kKgSplitLanes;
+// wave pairs (one Alice wave, one shuffle wave) per workgroup
+#ifndef QKD_KG_PAIRS
+#define QKD_KG_PAIRS 1
+#endif
+constexpr uint32_t kKgPairs = QKD_KG_PAIRS;
+constexpr uint32_t kKgBlock = 128 * kKgPairs;
+constexpr uint32_t kKgSplitFrames = kKgPairs * (64 / kKgSplitLanes);
 static_assert(kKgSplitLanes >= 1 && 64 % kKgSplitLanes == 0, "lanes per frame divide a wave");
 
 // Device-resident, immutable view of H.
