@@ -1570,7 +1570,8 @@ __global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCo
                                                                         uint32_t n_frames, uint32_t lsign,
                                                                         uint32_t* synw, uint32_t* counter) {
     extern __shared__ uint32_t T[];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // (uniform to the compiler)
     constexpr uint32_t NW = kSlicedBlock / 64;
     if (blockIdx.x == 0 && tid < 2) counter[tid] = 0;     // (the decoder's queue, as frame_syn_kernel)
     const uint32_t f0 = blockIdx.x * kSlicedFrames;
