@@ -1025,7 +1025,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             xunc[w] = 0;
         }
         __syncthreads();
-        const uint32_t f = ctl[1];
+        const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl[1]);   // (uniform to the compiler)
         if (f >= a.n_frames) break;
         if (tid == 0) next_f = atomicAdd(a.counter, 1u);
         // this launch's replays so far (read now, used for the next frame)
