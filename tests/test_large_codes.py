@@ -137,14 +137,14 @@ def test_large_code_variants_decode(Q, big_codes, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dv,dc", [(3, 6), (3, 12), (2, 16)])
-def test_frame_syn_sliced_equals_plain(monkeypatch, dv, dc):
+@pytest.mark.parametrize("dv,dc,n", [(3, 6, 2400), (3, 12, 2400), (2, 16, 2400), (3, 6, 2460)])
+def test_frame_syn_sliced_equals_plain(monkeypatch, dv, dc, n):
     """frame_syn_sliced_kernel (frames bit-sliced, uint16 check rows of width
     8 or 16) against frame_syn_kernel (QKD_SYN_SLICED=0): the
     same decoded words, iterations and flags on the keys path."""
     import torch
     import qkd_ldpc_amd as Q
-    n = 2400
+    # (N = 2460: an odd number of key words, the last slice pair half empty)
     m, cp, ci = regular_code(n, dv, dc, seed=dc)
     H = Q.HMatrix.from_check_lists(n, cp, ci)
     seeds = torch.from_numpy(Q.make_seeds(99, 600).view(np.int64)).cuda()
