@@ -1178,15 +1178,31 @@ __global__ __launch_bounds__(1024) void counters_one_kernel(const uint32_t* iter
     __syncthreads();
     unsigned long long c1 = 0, c2 = 0, c3 = 0, c4 = 0;
     uint32_t mn = 0xffffffffu, mx = 0;
-    for (uint32_t f = threadIdx.x; f < n_frames; f += blockDim.x) {
-        if (sp[f]) {
-            const unsigned long long it = iters[f];
-            c1++;
-            if (!ko || ko[f]) c2++;
-            c3 += it;
-            c4 += it * it;
-            mn = min(mn, (uint32_t)it);
-            mx = max(mx, (uint32_t)it);
+    // (every load unconditional and kCntBatch frames' loads issued together:
+    // a load behind the sp[f] branch made each frame two dependent round trips)
+    constexpr uint32_t kCntBatch = 4;
+    for (uint32_t f0 = threadIdx.x; f0 < n_frames; f0 += kCntBatch * blockDim.x) {
+        uint32_t itv[kCntBatch];
+        uint8_t spv[kCntBatch], kov[kCntBatch];
+#pragma unroll
+        for (uint32_t u = 0; u < kCntBatch; ++u) {
+            const uint32_t f = f0 + u * blockDim.x;
+            const bool in = f < n_frames;
+            itv[u] = in ? iters[f] : 0u;
+            spv[u] = in ? sp[f] : (uint8_t)0;
+            kov[u] = (in && ko) ? ko[f] : (uint8_t)1;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kCntBatch; ++u) {
+            if (spv[u]) {
+                const unsigned long long it = itv[u];
+                c1++;
+                if (kov[u]) c2++;
+                c3 += it;
+                c4 += it * it;
+                mn = min(mn, (uint32_t)it);
+                mx = max(mx, (uint32_t)it);
+            }
         }
     }
     // wave reductions first: one LDS atomic per wave and quantity
