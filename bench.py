@@ -338,7 +338,7 @@ def config4(args, H, Q, dev, rank, world):
     synchronize on both sides, max over ranks; an untimed run of the same shard first
     (workspace allocation, clocks). value = F * N bits / that time."""
     import torch
-    from qkd_ldpc_amd.dist import run_sharded_point
+    from qkd_ldpc_amd.dist import imbalance, run_sharded_point
     F = args.config4_frames
     ws = Q.Workspace(H)
     res = {}
@@ -353,7 +353,7 @@ def config4(args, H, Q, dev, rank, world):
                          out=res["r"])
         return res["r"].counters
 
-    counters, dt, (b, e) = run_sharded_point(rank, world, F, run_shard, torch.cuda.synchronize)
+    counters, dt, (b, e), per_rank = run_sharded_point(rank, world, F, run_shard, torch.cuda.synchronize)
     c = Q.read_counters(counters)
     q = float(res["r"].exact_qber[0].item())
     ws.close()
@@ -365,6 +365,7 @@ def config4(args, H, Q, dev, rank, world):
     return {"what": f"configs[3]: {F} config-2 frames over {world} rank(s), one qkd_trials_batch per rank "
                     "(keygen + decode + counters), counters all-reduced, max-rank time",
             "frames": F, "n_gpus": world, "frames_per_rank": e - b, "ms": dt * 1e3,
+            "per_rank_ms": [t * 1e3 for t in per_rank], "imbalance_max_over_min": imbalance(per_rank),
             "value": F * N_BITS / dt, "unit": "bit/s", "fer": st["fer"],
             "sum_iterations": got["sum_iters"], "mean_iterations": st["iterations_successful_sp_mean"],
             "std_iterations": st["iterations_successful_sp_std_dev"], "counters": got,
@@ -454,7 +455,7 @@ def main():
 
     H, g = load_code(torch.cuda.current_device())
     dev = torch.device("cuda", torch.cuda.current_device())
-    from qkd_ldpc_amd.dist import allreduce_counters, shard_range
+    from qkd_ldpc_amd.dist import allreduce_counters, imbalance, rank_times, shard_range
     F = args.frames
     all_seeds = Q.make_seeds(args.seed, F * world)
     b, e = shard_range(rank, world, F * world)          # weak scaling: F frames per rank
@@ -514,6 +515,7 @@ def main():
     for k in range(args.steps):
         step()
     torch.cuda.synchronize()
+    own_elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -524,10 +526,10 @@ def main():
         for k in range(3):
             step()
         dec_ms = decoder_ms(L, ws, False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # every rank's own time, barrier-inclusive time and decoder-kernel time in one
+    # all-gather: the max is the job's time, the spread its load imbalance
+    per_rank = rank_times([own_elapsed, elapsed, dec_ms or 0.0], world)
+    elapsed = max(r[1] for r in per_rank)
     # the whole library call (pack, frame syndromes, decoder), HIP events around it,
     # in a short untimed pass after the timed region
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
@@ -588,6 +590,15 @@ def main():
                         "decision, decoded again exactly (outputs bit-exact either way)",
             },
         }
+        if world > 1:
+            out["per_rank"] = {
+                "step_ms": [r[0] * 1e3 / args.steps for r in per_rank],
+                "decoder_kernel_ms": [r[2] for r in per_rank],
+                "imbalance_step": imbalance([r[0] for r in per_rank]),
+                "imbalance_decoder": imbalance([r[2] for r in per_rank]) if all(r[2] for r in per_rank) else None,
+                "note": "each rank's own timed loop (before the closing barrier) and its mean decoder "
+                        "kernel time (HIP events); imbalance = max / min",
+            }
         if os.environ.get("QKD_PHASE_TIMING"):
             cyc = np.zeros(7, np.uint64)
             Q._native.check(L.qkd_debug_phase_cycles(ws.handle, cyc.ctypes.data))

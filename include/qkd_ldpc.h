@@ -224,6 +224,14 @@ QKD_API qkd_status qkd_counters_batch(const uint32_t *iterations, const uint8_t 
                               const uint8_t *keys_match, size_t n_frames, qkd_counters *counters,
                               int device, void *stream);
 
+/* Combination of n_records counter records (device memory, e.g. one per rank
+ * after an all-gather) into *out (device memory; may alias a record): the
+ * reduction the reference's single process performs over every trial of a
+ * point (simulation.cpp:252-312) -- sums add, min_iters / max_iters take the
+ * minimum / maximum. One launch on `stream`. */
+QKD_API qkd_status qkd_counters_merge(const qkd_counters *records, size_t n_records, qkd_counters *out,
+                                      int device, void *stream);
+
 /* ---- diagnostics ------------------------------------------------------------
  * With QKD_PHASE_TIMING set in the environment, decode launches on `ws`
  * accumulate shader-clock cycles per phase, summed over workgroups (thread 0

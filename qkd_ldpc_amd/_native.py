@@ -64,6 +64,7 @@ EXPORTS = [
     "qkd_qber_range", "qkd_debug_phase_cycles", "qkd_debug_spec_replays", "qkd_debug_math", "qkd_debug_phi_sweep", "qkd_trace_decode",
     "qkd_interactive_batch",
     "qkd_code_from_alist_ex", "qkd_debug_decoder_timing", "qkd_debug_bit_order",
+    "qkd_counters_merge",
 ]
 
 
@@ -123,6 +124,7 @@ def lib():
             "qkd_keygen_batch": (st, [P, P, P, U64, SZ, D, P, P, P, P]),
             "qkd_trials_batch": (st, [P, P, P, U64, SZ, D, U32, D, U32, P, P, P, P, P, P]),
             "qkd_counters_batch": (st, [P, P, P, SZ, P, C.c_int, P]),
+            "qkd_counters_merge": (st, [P, SZ, P, C.c_int, P]),
             "qkd_make_seeds": (st, [U64, SZ, P]),
             "qkd_qber_range": (st, [D, D, D, P, SZ, C.POINTER(SZ)]),
             "qkd_debug_phase_cycles": (st, [P, P]),

@@ -1256,6 +1256,42 @@ static hipError_t launch_counters(const uint32_t* iters, const uint8_t* sp, cons
     return hipGetLastError();
 }
 
+// The records of n ranks (one all-gather, qkd_ldpc_amd/dist.py) combined as the
+// reference's one-process reduction would see all their frames
+// (simulation.cpp:252-312): sums add, extrema take min / max. One wave; every
+// record is read before `out` is written, so `out` may alias any of them.
+__global__ __launch_bounds__(64) void counters_merge_kernel(const qkd_counters* recs, uint32_t n,
+                                                            qkd_counters* out) {
+    unsigned long long s[5] = {0, 0, 0, 0, 0};
+    uint32_t mn = 0xffffffffu, mx = 0;
+    for (uint32_t r = threadIdx.x; r < n; r += 64) {
+        const qkd_counters c = recs[r];
+        s[0] += c.frames;
+        s[1] += c.sp_ok;
+        s[2] += c.ldpc_ok;
+        s[3] += c.sum_iters;
+        s[4] += c.sum_iters_sq;
+        mn = min(mn, c.min_iters);
+        mx = max(mx, c.max_iters);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s[k] += __shfl_xor(s[k], o);
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out->frames = s[0];
+        out->sp_ok = s[1];
+        out->ldpc_ok = s[2];
+        out->sum_iters = s[3];
+        out->sum_iters_sq = s[4];
+        out->min_iters = mn;
+        out->max_iters = mx;
+    }
+}
+
 // ---- launch plumbing --------------------------------------------------------
 
 
@@ -2450,6 +2486,18 @@ qkd_status qkd_counters_batch(const uint32_t* iterations, const uint8_t* syndrom
     if (s != QKD_OK) return s;
     DeviceGuard g(device);
     QKD_HIP(launch_counters(iterations, syndromes_match, keys_match, n_frames, counters, (hipStream_t)stream));
+    return QKD_OK;
+}
+
+qkd_status qkd_counters_merge(const qkd_counters* records, size_t n_records, qkd_counters* out, int device,
+                              void* stream) {
+    clear_error();
+    if (!records || !out) return set_error(QKD_ERR_INVALID_ARG, "null argument");
+    if (n_records == 0 || n_records > 0xffffffffu) return set_error(QKD_ERR_INVALID_ARG, "bad record count");
+    DeviceGuard g(device);
+    hipLaunchKernelGGL(counters_merge_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, records,
+                       (uint32_t)n_records, out);
+    QKD_HIP(hipGetLastError());
     return QKD_OK;
 }
 

@@ -3,10 +3,11 @@
 One process per GPU. Every rank derives the same seed stream
 (simulation.cpp:222-228) and takes a contiguous frame range; nothing is
 exchanged on the data path. The per-point counters of simulation.cpp:252-312
-(frames, sp_ok, ldpc_ok, Σit, Σit², min it, max it) are combined with one
-all-reduce each for the sums (SUM) and the extrema (MIN / MAX), over RCCL on
-MI355X (backend "nccl") or gloo on CPU. The integer sums make the combined
-mean/std independent of the rank count.
+(frames, sp_ok, ldpc_ok, Σit, Σit², min it, max it) are combined with ONE
+collective per step: an all-gather of the 48-byte records (RCCL on MI355X,
+backend "nccl"; gloo on CPU), then one merge launch on the device
+(qkd_counters_merge: sums add, extrema min / max). The integer sums make the
+combined mean/std independent of the rank count.
 
 This replaces the reference's thread-pool fan-out of a point's trials
 (simulation.cpp:230-250, `detach_loop` over THREADS_NUMBER threads): ranks
@@ -38,22 +39,60 @@ def shard_range(rank: int, world: int, frames: int) -> tuple[int, int]:
     return begin, begin + base + (1 if rank < extra else 0)
 
 
-def allreduce_counters(counters, group=None):
-    """In-place all-reduce of a qkd_counters record held as a uint8 tensor
-    (layout of include/qkd_ldpc.h: 5 x uint64 sums, then uint32 min, uint32 max)."""
+COUNTERS_BYTES = 48       # sizeof(qkd_counters), include/qkd_ldpc.h
+
+
+def gather_records(rec, group=None):
+    """One all-gather of every rank's `rec` (a 1-D tensor of the same size and
+    dtype on every rank): returns a [world, rec.numel()] tensor, row r = rank r's
+    record. The only collective of a step (RCCL on MI355X, gloo on CPU)."""
     import torch
     import torch.distributed as dist
 
-    words = counters.view(torch.int64)              # 6 words: 5 sums + (min | max << 32)
-    sums = words[:5]
-    ext = counters[40:48].view(torch.int32)         # [min, max]
-    mn = ext[0:1].to(torch.int64) & 0xFFFFFFFF      # uint32 -> non-negative int64
-    mx = ext[1:2].to(torch.int64) & 0xFFFFFFFF
-    dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-    ext[0:1] = mn.to(torch.int32)                   # two's-complement store keeps the uint32 bits
-    ext[1:2] = mx.to(torch.int32)
+    world = dist.get_world_size(group)
+    src = rec.contiguous()
+    if rec.is_cuda and dist.get_backend(group) == "gloo":
+        src = src.cpu()              # gloo rehearsals on one device: host staging
+    out = torch.empty(world * src.numel(), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out.view(world, src.numel()).to(rec.device)
+
+
+def merge_counters(records, out):
+    """records: [n, 48] uint8 rows, each a qkd_counters record (include/qkd_ldpc.h:
+    5 x uint64 sums, uint32 min, uint32 max) -> their combination in `out` (48
+    bytes, may be a view of a row): sums add, extrema take min / max, the
+    reduction of simulation.cpp:252-312 over the union of the ranks' frames.
+    Device tensors: one qkd_counters_merge launch (the library's kernel) on the
+    current stream. Host tensors (the gloo rehearsals on CPU): the same in numpy."""
+    import numpy as np
+    import torch
+
+    n = records.shape[0]
+    if records.is_cuda:
+        from . import _native as N
+        import ctypes
+
+        recs = records.contiguous()
+        N.check(N.lib().qkd_counters_merge(ctypes.c_void_p(recs.data_ptr()), n,
+                                           ctypes.c_void_p(out.data_ptr()), out.device.index,
+                                           ctypes.c_void_p(torch.cuda.current_stream(out.device).cuda_stream)))
+        return out
+    a = records.contiguous().numpy().reshape(n, COUNTERS_BYTES)
+    sums = a[:, :40].copy().view(np.uint64).sum(axis=0, dtype=np.uint64)
+    ext = a[:, 40:48].copy().view(np.uint32)
+    rec = np.zeros(COUNTERS_BYTES, np.uint8)
+    rec[:40] = sums.view(np.uint8)
+    rec[40:48] = np.array([ext[:, 0].min(), ext[:, 1].max()], np.uint32).view(np.uint8)
+    out.copy_(torch.from_numpy(rec))
+    return out
+
+
+def allreduce_counters(counters, group=None):
+    """In-place all-reduce of a qkd_counters record held as a uint8 tensor: ONE
+    all-gather of the 48-byte records, then their merge on the device
+    (qkd_counters_merge). Every rank ends with the same record."""
+    merge_counters(gather_records(counters, group), counters)
     return counters
 
 
@@ -65,10 +104,11 @@ def run_sharded_point(rank: int, world: int, frames: int, run_shard, sync=None):
     run_shard(begin, end) runs this rank's frames [begin, end) of the shared seed
     stream and returns its qkd_counters record (uint8 tensor, 48 bytes, on the
     rank's device). It is called twice: once untimed (allocation, clocks), then
-    timed between a barrier + sync() on both sides. The records are all-reduced
-    (SUM / MIN / MAX) and the time is the max over ranks. Every rank must call
-    this (it issues collectives when world > 1). Returns (counters, seconds,
-    (begin, end))."""
+    timed between a barrier + sync() on both sides. One all-gather then carries
+    every rank's record and its own time: the records are merged (SUM / MIN /
+    MAX) and the time is the max over ranks. Every rank must call this (it
+    issues collectives when world > 1). Returns (counters, seconds, (begin,
+    end), per_rank_seconds)."""
     import torch
     import torch.distributed as dist
 
@@ -82,15 +122,42 @@ def run_sharded_point(rank: int, world: int, frames: int, run_shard, sync=None):
     t0 = time.perf_counter()
     counters = run_shard(b, e)
     sync()
+    rank_dt = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    per_rank = [rank_dt]
     if world > 1:
-        allreduce_counters(counters)
-        t = torch.tensor([dt], dtype=torch.float64, device=counters.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    return counters, dt, (b, e)
+        # [48-byte record | this rank's own time (binary64) | its barrier-inclusive time]
+        rec = torch.empty(COUNTERS_BYTES + 16, dtype=torch.uint8, device=counters.device)
+        rec[:COUNTERS_BYTES] = counters
+        rec[COUNTERS_BYTES:] = torch.tensor([rank_dt, dt], dtype=torch.float64).view(torch.uint8).to(
+            counters.device)
+        g = gather_records(rec)
+        merge_counters(g[:, :COUNTERS_BYTES], counters)
+        t = g[:, COUNTERS_BYTES:].contiguous().view(torch.float64).view(world, 2).cpu()
+        per_rank = [float(x) for x in t[:, 0]]
+        dt = float(t[:, 1].max())
+    return counters, dt, (b, e), per_rank
+
+
+def rank_times(values, world):
+    """All ranks' float values (e.g. their step time and decoder time) in one
+    all-gather: returns a [world][len(values)] list (every rank gets it)."""
+    import torch
+
+    if world == 1:
+        return [list(map(float, values))]
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    g = gather_records(torch.tensor([float(v) for v in values], dtype=torch.float64, device=dev))
+    return [[float(x) for x in row] for row in g.cpu()]
+
+
+def imbalance(per_rank):
+    """max / min of per-rank times (1.0 = perfectly balanced)."""
+    lo = min(per_rank)
+    return max(per_rank) / lo if lo > 0 else None
 
 
 def free_port() -> int:

@@ -45,10 +45,10 @@ def main():
                                                 np.asarray(r["sp_ok"], np.uint8),
                                                 np.asarray(r["key_ok"], np.uint8)))
 
-        rec, dt, (b, e) = run_sharded_point(rank, world, frames, run_shard)
+        rec, dt, (b, e), per_rank = run_sharded_point(rank, world, frames, run_shard)
         t = torch.tensor([float(e - b)], dtype=torch.float64)
         dist.all_reduce(t)
-        extra = {"seconds": dt}
+        extra = {"seconds": dt, "per_rank_seconds": per_rank}
     else:
         b, e = shard_range(rank, world, frames)
         r = code.trials(q, seeds[b:e], 0, 50, 100.0, True, threads=2)

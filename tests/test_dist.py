@@ -50,7 +50,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_counter_allreduce_matches_single_process(world):
     rng = np.random.default_rng(0)
     f = 1001
@@ -122,11 +122,33 @@ def test_bench_gpus_two_without_gpus_fails_loudly():
     assert "no visible GPU" in p.stderr
 
 
-def test_config4_point_over_two_ranks_matches_fixture(tmp_path):
-    """bench.py's configs[3] path (dist.run_sharded_point) on two gloo ranks, the oracle
-    decoding each rank's shard of the first 40 config-4 frames: the all-reduced record
+def test_merge_counters_host_form():
+    """dist.merge_counters on host records (the gloo path): sums add, min / max of the
+    extrema, the identities of an all-failed record (UINT32_MAX / 0) neutral."""
+    from qkd_ldpc_amd.dist import merge_counters
+    rng = np.random.default_rng(3)
+    recs = []
+    for k in range(5):
+        f = 50 + k
+        it = rng.integers(2, 51, f).astype(np.uint32)
+        sp = (rng.random(f) < (0.0 if k == 2 else 0.9)).astype(np.uint8)
+        ko = (rng.random(f) < 0.9).astype(np.uint8)
+        recs.append((it, sp, ko))
+    rows = np.stack([counters_of(*r) for r in recs])
+    out = torch.empty(48, dtype=torch.uint8)
+    merge_counters(torch.from_numpy(rows), out)
+    want = counters_of(np.concatenate([r[0] for r in recs]), np.concatenate([r[1] for r in recs]),
+                       np.concatenate([r[2] for r in recs]))
+    assert out.numpy().tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_config4_point_over_ranks_matches_fixture(tmp_path, world):
+    """bench.py's configs[3] path (dist.run_sharded_point: ONE all-gather of every
+    rank's record and time) on 2 and 4 gloo ranks started by spawn_ranks, the oracle
+    decoding each rank's shard of the first 40 config-4 frames: the merged record
     equals the config-4 fixture's counters over the same frames (bench.py
-    config4_fixture_counters), and the time is reported."""
+    config4_fixture_counters), and every rank's time is reported."""
     import json
     import sys
     from qkd_ldpc_amd.dist import spawn_ranks
@@ -134,7 +156,7 @@ def test_config4_point_over_two_ranks_matches_fixture(tmp_path):
     from bench import config4_fixture_counters
     out = str(tmp_path / "c4.json")
     frames = 40
-    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "dist_rehearsal.py"), out, str(frames), "0.02"],
+    rc = spawn_ranks(world, [os.path.join(ROOT, "tests", "dist_rehearsal.py"), out, str(frames), "0.02"],
                      env_extra={"QKD_REHEARSAL": "point"})
     assert rc == 0
     got = json.load(open(out))
@@ -142,7 +164,8 @@ def test_config4_point_over_two_ranks_matches_fixture(tmp_path):
     sums = rec[:40].view(np.uint64)
     ext = rec[40:48].view(np.uint32)
     want = config4_fixture_counters(frames)
-    assert got["frames"] == frames and got["seconds"] > 0
+    assert got["frames"] == frames and got["seconds"] > 0 and got["world"] == world
+    assert len(got["per_rank_seconds"]) == world and got["seconds"] >= max(got["per_rank_seconds"])
     assert [int(x) for x in sums] == [want["frames"], want["sp_ok"], want["ldpc_ok"], want["sum_iters"],
                                       want["sum_iters_sq"]]
     assert [int(ext[0]), int(ext[1])] == [want["min_iters"], want["max_iters"]]

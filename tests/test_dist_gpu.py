@@ -71,3 +71,27 @@ def test_bench_config4_over_two_ranks():
     assert c4["matches_fixture"] is True, c4["counters"]
     assert c4["counters"]["frames"] == frames and c4["fer"] == 0.0
     assert abs(c4["value"] - frames * 10240 / (c4["ms"] / 1e3)) / c4["value"] < 1e-9
+
+
+def test_counters_merge_kernel_matches_host_form():
+    """qkd_counters_merge (the device half of dist.allreduce_counters: one launch after
+    the all-gather) against the host form on eight records, one of them all-failed
+    (UINT32_MAX / 0 extrema), the output aliasing the first record."""
+    import torch
+    from qkd_ldpc_amd.dist import merge_counters
+    from test_dist import counters_of
+    rng = np.random.default_rng(11)
+    rows = []
+    for k in range(8):
+        f = 100 + 7 * k
+        it = rng.integers(1, 51, f).astype(np.uint32)
+        sp = (rng.random(f) < (0.0 if k == 5 else 0.8)).astype(np.uint8)
+        ko = (rng.random(f) < 0.9).astype(np.uint8)
+        rows.append(counters_of(it, sp, ko))
+    host = torch.from_numpy(np.stack(rows))
+    want = torch.empty(48, dtype=torch.uint8)
+    merge_counters(host, want)
+    dev = host.cuda()
+    merge_counters(dev, dev[0])
+    torch.cuda.synchronize()
+    assert dev[0].cpu().numpy().tobytes() == want.numpy().tobytes()
