@@ -661,6 +661,20 @@ __global__ void pack_kernel(const uint8_t* bytes0, const uint8_t* bytes1, uint32
     reinterpret_cast<uint8_t*>(out)[gid] = (uint8_t)m;
 }
 
+hipError_t launch_pack_keys(const DecodeArgs& a, hipStream_t stream) {
+    const uint32_t n = (uint32_t)a.code.n;
+    const size_t nw = (size_t)a.n_frames * a.words;
+    // Alice's and Bob's keys in one launch (grid.y selects the key; the wide
+    // form needs both arrays 16-byte aligned)
+    const bool wide = (n % 32) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(a.alice_b) | reinterpret_cast<uintptr_t>(a.bob_b)) & 15u) == 0;
+    const size_t threads = wide ? nw * 2 : nw * 8;
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((threads + 255) / 256), 2), dim3(256), 0, stream,
+                       a.alice_b, a.bob_b, n, a.words, a.n_frames, const_cast<uint64_t*>(a.alice_w),
+                       const_cast<uint64_t*>(a.bob_w), wide ? 1u : 0u);
+    return hipGetLastError();
+}
+
 __global__ void unpack_kernel(const uint64_t* words_in, uint32_t n, uint32_t words, uint32_t n_frames,
                               uint8_t* out) {
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1499,13 +1513,18 @@ static unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 
 static constexpr size_t kDecEvPairsMax = 256;
 static hipError_t decoder_events_fold(qkd_workspace* ws) {
     const size_t pairs = ws->dec_ev_used / 2;
+    // summed locally and committed only once every pair has been read: a failure
+    // part-way leaves the totals and the pool as they were (a retry folds the
+    // same pairs once, not twice)
+    double ms_sum = 0.0;
     for (size_t k = 0; k < pairs; ++k) {
         hipError_t r = hipEventSynchronize(ws->dec_ev[2 * k + 1]);
         float ms = 0.0f;
         if (r == hipSuccess) r = hipEventElapsedTime(&ms, ws->dec_ev[2 * k], ws->dec_ev[2 * k + 1]);
         if (r != hipSuccess) return r;
-        ws->dec_ms_folded += ms;
+        ms_sum += ms;
     }
+    ws->dec_ms_folded += ms_sum;
     ws->dec_pairs_folded += pairs;
     ws->dec_ev_used = 0;
     return hipSuccess;
@@ -1675,17 +1694,6 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             }
             a.replay_count = ws->counter + 1;
             a.spec_replays = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 120);
-            // [0] frame queue, [1] replays: zeroed by frame_syn_kernel on the
-            // keys path (it runs first on this stream: block 0 writes both
-            // words), by a memset otherwise -- one branch, so a keys-mode
-            // launch without frame_syn cannot exist
-            if (mode == kModeKeys) {
-                a.synw = ws->synw;
-                a.zout = ws->zout;
-                QKD_HIP(launch_frame_syn(a, stream));
-            } else {
-                QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));
-            }
             if (spec) {
                 int xdc = 0, sgrid = 0;
                 DecodeFn xfn = pick_split_spec(mode, c->max_dc, ckpt, &xdc);
@@ -1715,6 +1723,20 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 s = check_no_static_lds(sfn);
                 if (s != QKD_OK) return s;
             }
+            // [0] frame queue, [1] replays: zeroed by frame_syn_kernel on the
+            // keys path (it runs first on this stream: block 0 writes both
+            // words), by a memset otherwise -- one branch, so a keys-mode
+            // launch without frame_syn cannot exist. Every check that can fail
+            // comes before it: frame_syn rewrites ws->alice_w / bob_w in place
+            // in the internal bit order, and after it only the decoder (which
+            // reads them in that order) may follow.
+            if (mode == kModeKeys) {
+                a.synw = ws->synw;
+                a.zout = ws->zout;
+                QKD_HIP(launch_frame_syn(a, stream));
+            } else {
+                QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));
+            }
             QKD_HIP(decoder_event(ws, stream));
             hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
             QKD_HIP(decoder_event_close(ws, stream, hipGetLastError()));
@@ -1722,6 +1744,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             return QKD_OK;
         }
     }
+    // (byte keys: the classic kernel reads them packed, in the original order)
+    if (mode == kModeKeys && a.alice_b) QKD_HIP(launch_pack_keys(a, stream));
     const bool gt = decode_needs_gt(c, rule, a.tab2_entries);
     if (gt) {                                     // large code: no per-bit LDS tables
         a.first_table = 0;
@@ -1877,8 +1901,11 @@ static SpecClean& spec_clean_of(qkd_workspace* ws, double q) {
 // Shared by qkd_qkd_ldpc_batch and qkd_trials_batch: keys already packed in ws.
 static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_frames, double q,
                               uint32_t max_it, double thr, uint32_t flags, uint8_t* bits_out,
-                              uint32_t* iters, uint8_t* sp_ok, uint8_t* key_ok, hipStream_t stream) {
+                              uint32_t* iters, uint8_t* sp_ok, uint8_t* key_ok, hipStream_t stream,
+                              const uint8_t* alice_b = nullptr, const uint8_t* bob_b = nullptr) {
     DecodeArgs a{};
+    a.alice_b = alice_b;
+    a.bob_b = bob_b;
     a.pinf = std::numeric_limits<float>::infinity();
     a.n_frames = (uint32_t)n_frames;
     a.max_it = max_it;
@@ -1984,17 +2011,10 @@ qkd_status qkd_qkd_ldpc_batch(const qkd_code* c, qkd_workspace* ws, const uint8_
     WsSession sess(ws, (hipStream_t)stream);
     s = ws_reserve_keys(ws, n_frames, 1);
     if (s != QKD_OK) return s;
-    const uint32_t words = (uint32_t)((c->n + 63) / 64);
-    const size_t nw = n_frames * words;
-    // Alice's and Bob's keys in one launch (grid.y selects the key; the wide
-    // form needs both arrays 16-byte aligned)
-    const bool wide = (c->n % 32) == 0 && ((reinterpret_cast<uintptr_t>(alice) | reinterpret_cast<uintptr_t>(bob)) & 15u) == 0;
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks_for(wide ? nw * 2 : nw * 8, 256), 2), dim3(256), 0, (hipStream_t)stream,
-                       alice, bob, (uint32_t)c->n, words, (uint32_t)n_frames, ws->alice_w, ws->bob_w,
-                       wide ? 1u : 0u);
-    QKD_HIP(hipGetLastError());
+    // the byte keys go to the decode launch, which packs them (the split
+    // path inside its frame-syndrome kernel, launch_frame_syn)
     return decode_keys(c, ws, n_frames, qber, max_iterations, msg_threshold, flags, bits_out, iterations,
-                       syndromes_match, keys_match, (hipStream_t)stream);
+                       syndromes_match, keys_match, (hipStream_t)stream, alice, bob);
 }
 
 static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uint64_t* seeds,

@@ -1565,10 +1565,20 @@ constexpr int kSlicedPre = 8;        // key-word pairs a wave loads ahead
 __device__ __forceinline__ uint64_t put_lane(uint64_t x, uint32_t at, uint64_t m) {
     return (threadIdx.x & 63u) == at ? m : x;
 }
+// BYTES (qkd_qkd_ldpc_batch's byte keys, N % 8 == 0, rows 8-byte aligned): the
+// slices come straight from the caller's 0/1 bytes, and alice_w / bob_w are
+// only written (step 3), so no packing kernel runs before this one: per
+// thread and pass 8 positions of every frame and key, one 8-byte load each;
+// (v & 0x01010101) << f gathers 8 frames' bits of 4 positions into the 4
+// bytes of one word, and v_perm_b32 assembles each position's slice from the
+// four words (Alice frames 0-7 / 8-15, Bob frames 0-7 / 8-15).
+template <bool BYTES>
 __global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCode c, uint64_t* alice_w,
                                                                         uint64_t* bob_w, uint32_t words,
                                                                         uint32_t n_frames, uint32_t lsign,
-                                                                        uint32_t* synw, uint32_t* counter) {
+                                                                        uint32_t* synw, uint32_t* counter,
+                                                                        const uint8_t* alice_b,
+                                                                        const uint8_t* bob_b) {
     extern __shared__ uint32_t T[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // (uniform to the compiler)
@@ -1603,13 +1613,49 @@ __global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCo
         T[(size_t)(2 * p) * 64 + lane] = (uint32_t)mine;
         if (2 * p + 1 < words) T[(size_t)(2 * p + 1) * 64 + lane] = (uint32_t)(mine >> 32);
     };
-    for (uint32_t p0 = wave; p0 < pairs; p0 += NW * kSlicedPre) {
-        uint64_t v[kSlicedPre];
+    if constexpr (BYTES) {
+        const uint32_t n = (uint32_t)c.n;
+        for (uint32_t p = tid; p * 8 < n; p += kSlicedBlock) {
+            uint2 va[kSlicedFrames], vb[kSlicedFrames];
 #pragma unroll
-        for (int k = 0; k < kSlicedPre; ++k) v[k] = load_pair(p0 + (uint32_t)k * NW);
+            for (uint32_t f = 0; f < (uint32_t)kSlicedFrames; ++f) {
+                const size_t off = (size_t)(f0 + f) * n + 8 * p;
+                va[f] = f < nf ? *reinterpret_cast<const uint2*>(alice_b + off) : make_uint2(0, 0);
+                vb[f] = f < nf ? *reinterpret_cast<const uint2*>(bob_b + off) : make_uint2(0, 0);
+            }
+            // x[key][frame half][position half]: byte k bit f' = that key's bit
+            // at position 4 * (position half) + k of frame 8 * (frame half) + f'
+            uint32_t x[2][2][2] = {};
 #pragma unroll
-        for (int k = 0; k < kSlicedPre; ++k)
-            if (p0 + (uint32_t)k * NW < pairs) slice_pair(p0 + (uint32_t)k * NW, v[k]);
+            for (uint32_t f = 0; f < (uint32_t)kSlicedFrames; ++f) {
+                const uint32_t h = f >> 3, sh = f & 7u;
+                x[0][h][0] |= (va[f].x & 0x01010101u) << sh;
+                x[0][h][1] |= (va[f].y & 0x01010101u) << sh;
+                x[1][h][0] |= (vb[f].x & 0x01010101u) << sh;
+                x[1][h][1] |= (vb[f].y & 0x01010101u) << sh;
+            }
+            uint32_t sl[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t ph = k >> 2, b = k & 3u;
+                // bytes 0-1: Alice frames 0-7 / 8-15; 2-3: Bob's (selector 12: 0x00)
+                const uint32_t lo = __builtin_amdgcn_perm(x[0][1][ph], x[0][0][ph], b | ((b + 4) << 8) | 0x0c0c0000u);
+                const uint32_t hi = __builtin_amdgcn_perm(x[1][1][ph], x[1][0][ph], 0x0c0cu | (b << 16) | ((b + 4) << 24));
+                sl[k] = lo | hi;
+            }
+            // (positions past N are never read: rows and perm hold bits < N)
+            *reinterpret_cast<uint4*>(T + 8 * p) = make_uint4(sl[0], sl[1], sl[2], sl[3]);
+            *reinterpret_cast<uint4*>(T + 8 * p + 4) = make_uint4(sl[4], sl[5], sl[6], sl[7]);
+        }
+    } else {
+        for (uint32_t p0 = wave; p0 < pairs; p0 += NW * kSlicedPre) {
+            uint64_t v[kSlicedPre];
+#pragma unroll
+            for (int k = 0; k < kSlicedPre; ++k) v[k] = load_pair(p0 + (uint32_t)k * NW);
+#pragma unroll
+            for (int k = 0; k < kSlicedPre; ++k)
+                if (p0 + (uint32_t)k * NW < pairs) slice_pair(p0 + (uint32_t)k * NW, v[k]);
+        }
     }
     __syncthreads();
     // 2. syndromes: lane = check; 64 checks per wave and pass, then per frame
@@ -1670,18 +1716,34 @@ hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
     // (QKD_SYN_SLICED=0: frame_syn_kernel; tests compare the two)
     const size_t slds = (size_t)a.words * 64 * sizeof(uint32_t);
     const char* se = getenv("QKD_SYN_SLICED");
-    if (a.code.chk_rows16 && slds <= 160 * 1024 && !(se && atoi(se) == 0)) {
-        static bool attr = false;
-        if (!attr) {
-            const hipError_t e = hipFuncSetAttribute((const void*)frame_syn_sliced_kernel,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
-        hipLaunchKernelGGL(frame_syn_sliced_kernel, dim3((a.n_frames + kSlicedFrames - 1) / kSlicedFrames),
-                           dim3(kSlicedBlock), slds, stream, a.code, const_cast<uint64_t*>(a.alice_w),
-                           const_cast<uint64_t*>(a.bob_w), a.words, a.n_frames, lsign,
-                           const_cast<uint32_t*>(a.synw), a.counter);
+    const bool sliced = a.code.chk_rows16 && slds <= 160 * 1024 && !(se && atoi(se) == 0);
+    // byte keys (qkd_qkd_ldpc_batch): packed by the sliced kernel itself when
+    // their rows allow 8-byte loads (QKD_SYN_BYTES=0: pack_kernel first; tests
+    // compare the two), else by pack_kernel
+    const char* sb = getenv("QKD_SYN_BYTES");
+    const bool bytes = a.alice_b && sliced && a.code.n % 8 == 0 &&
+                       ((reinterpret_cast<uintptr_t>(a.alice_b) | reinterpret_cast<uintptr_t>(a.bob_b)) & 7u) == 0 &&
+                       !(sb && atoi(sb) == 0);
+    if (a.alice_b && !bytes) {
+        const hipError_t e = launch_pack_keys(a, stream);
+        if (e != hipSuccess) return e;
+    }
+    if (sliced) {
+        const void* fn = bytes ? (const void*)frame_syn_sliced_kernel<true> : (const void*)frame_syn_sliced_kernel<false>;
+        // (the attribute on every launch, for the current device, as decode_grid
+        // does for the decoder: no process-wide flag to race on or to skip for
+        // a second device)
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        const dim3 grid((a.n_frames + kSlicedFrames - 1) / kSlicedFrames);
+        if (bytes)
+            hipLaunchKernelGGL(frame_syn_sliced_kernel<true>, grid, dim3(kSlicedBlock), slds, stream, a.code,
+                               const_cast<uint64_t*>(a.alice_w), const_cast<uint64_t*>(a.bob_w), a.words,
+                               a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter, a.alice_b, a.bob_b);
+        else
+            hipLaunchKernelGGL(frame_syn_sliced_kernel<false>, grid, dim3(kSlicedBlock), slds, stream, a.code,
+                               const_cast<uint64_t*>(a.alice_w), const_cast<uint64_t*>(a.bob_w), a.words,
+                               a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter, nullptr, nullptr);
         return hipGetLastError();
     }
     const size_t lds = (size_t)kSynFrames * 2 * a.words * sizeof(uint64_t);

@@ -186,19 +186,22 @@ static void internal_bit_order(int32_t n, int32_t n_pad, const std::vector<int32
     }
 }
 
-// Validate the check-side CSR, derive the bit side, upload the ELL layouts.
-static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* cptr,
-                             const int32_t* cidx, int device) {
+// The check-side CSR's invariants (qkd_code_create): cptr[0] = 0, monotone
+// offsets, at least one edge, bit indices in range, every row strictly
+// ascending (QKD_ERR_UNSORTED when a row descends: the reference would
+// silently mis-route its messages). Fills bdeg[n] (bit
+// degrees) and max_dc.
+static qkd_status validate_csr(int32_t n, int32_t m, const int32_t* cptr, const int32_t* cidx,
+                               std::vector<int32_t>& bdeg, int32_t& max_dc) {
     if (n <= 0 || m <= 0 || !cptr || !cidx)
         return set_error(QKD_ERR_INVALID_ARG, "qkd_code_create: n=%d m=%d, null adjacency", n, m);
     if (cptr[0] != 0) return set_error(QKD_ERR_BAD_CODE, "check_ptr[0] must be 0");
     for (int32_t j = 0; j < m; ++j)
         if (cptr[j + 1] < cptr[j])
             return set_error(QKD_ERR_BAD_CODE, "check_ptr not monotone at check %d", j);
-    const int32_t e = cptr[m];
-    if (e <= 0) return set_error(QKD_ERR_BAD_CODE, "code has no edges");
-    int32_t max_dc = 0;
-    std::vector<int32_t> bdeg(n, 0);
+    if (cptr[m] <= 0) return set_error(QKD_ERR_BAD_CODE, "code has no edges");
+    max_dc = 0;
+    bdeg.assign(n, 0);
     for (int32_t j = 0; j < m; ++j) {
         const int32_t d = cptr[j + 1] - cptr[j];
         max_dc = std::max(max_dc, d);
@@ -213,6 +216,17 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
             bdeg[b]++;
         }
     }
+    return QKD_OK;
+}
+
+// Validate the check-side CSR, derive the bit side, upload the ELL layouts.
+static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* cptr,
+                             const int32_t* cidx, int device) {
+    std::vector<int32_t> bdeg;
+    int32_t max_dc = 0;
+    qkd_status vs = validate_csr(n, m, cptr, cidx, bdeg, max_dc);
+    if (vs != QKD_OK) return vs;
+    const int32_t e = cptr[m];
     int32_t max_dv = 0;
     for (int32_t i = 0; i < n; ++i) max_dv = std::max(max_dv, bdeg[i]);
     if (max_dc > kMaxCheckDegree)
@@ -324,8 +338,15 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
                           hipMemcpyHostToDevice));
         QKD_HIP(hipMemcpy(c->d_pat_deg, c->pat_deg.data(), c->pat_deg.size(), hipMemcpyHostToDevice));
     }
-    // the split kernels' internal bit order (internal_bit_order)
+    // The split kernels' data (decode_split.hip), only for codes they take
+    // (N <= kMaxBitsSplit, M <= kMaxChecksSplit; the launcher checks the same):
+    // larger codes run the classic kernel on the original order, so the
+    // internal bit order (its bank pass searches up to 200k moves) and the
+    // internal-order arrays are neither computed nor uploaded for them.
+    const bool split = n <= kMaxBitsSplit && m <= kMaxChecksSplit;
     std::vector<int32_t> perm(n), inv(n, -1);
+    if (split) {
+    // the split kernels' internal bit order (internal_bit_order)
     internal_bit_order(n, c->n_pad, bdeg, plan, perm, inv, getenv("QKD_BIT_ORDER"));
     // the per-bit arrays in that order (the split kernels' DeviceCode view)
     std::vector<int32_t> bit_chk_s(bit_chk.size(), -1);
@@ -382,19 +403,22 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         QKD_HIP(hipMalloc(&c->d_bit_code, code.size() * sizeof(uint64_t)));
         QKD_HIP(hipMemcpy(c->d_bit_code, code.data(), code.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
     }
+    }   // split
     std::vector<uint2> plan2(plan.word.size());
     for (size_t k = 0; k < plan.word.size(); ++k) plan2[k] = make_uint2(plan.word[k], plan.seg[k]);
     QKD_HIP(hipMalloc(&c->d_plan, plan2.size() * sizeof(uint2)));
     QKD_HIP(hipMemcpy(c->d_plan, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    // the same plan slot-addressed for the split kernels (row * n_pad +
-    // internal bit; idle lanes: the dummy column n's slot)
-    for (size_t k = 0; k < plan.word.size(); ++k) {
-        const uint32_t b = plan.word[k] & qkdp::kPlanBitMask;
-        plan2[k].x = (plan.word[k] >> 24) * (uint32_t)c->n_pad + (b < (uint32_t)n ? (uint32_t)inv[b] : b);
+    if (split) {
+        // the same plan slot-addressed for the split kernels (row * n_pad +
+        // internal bit; idle lanes: the dummy column n's slot)
+        for (size_t k = 0; k < plan.word.size(); ++k) {
+            const uint32_t b = plan.word[k] & qkdp::kPlanBitMask;
+            plan2[k].x = (plan.word[k] >> 24) * (uint32_t)c->n_pad + (b < (uint32_t)n ? (uint32_t)inv[b] : b);
+        }
+        QKD_HIP(hipMalloc(&c->d_plan_slot, plan2.size() * sizeof(uint2)));
+        QKD_HIP(hipMemcpy(c->d_plan_slot, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
+        c->plan_slot_host = std::move(plan2);
     }
-    QKD_HIP(hipMalloc(&c->d_plan_slot, plan2.size() * sizeof(uint2)));
-    QKD_HIP(hipMemcpy(c->d_plan_slot, plan2.data(), plan2.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    c->plan_slot_host = std::move(plan2);
     // Key-generation jump-ahead: chunk = draws per lane, a multiple of 64 so
     // every lane's Alice bits fill whole words.
     const uint64_t draws = qkdr::trial_draws((uint32_t)n);
@@ -680,13 +704,13 @@ qkd_status qkd_code_get_adjacency(const qkd_code* c, int32_t* check_ptr, int32_t
 qkd_status qkd_debug_bit_order(int32_t n, int32_t m, const int32_t* cptr, const int32_t* cidx, const char* mode,
                                int32_t* perm_out, uint32_t* plan_out, int32_t* n_tasks_out) {
     clear_error();
-    if (n <= 0 || m <= 0 || !cptr || !cidx || !n_tasks_out) return set_error(QKD_ERR_INVALID_ARG, "bad arguments");
-    std::vector<int32_t> bdeg(n, 0), fill(n, 0), krow(cptr[m]);
-    for (int32_t j = 0; j < m; ++j)
-        for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) {
-            if (cidx[k] < 0 || cidx[k] >= n) return set_error(QKD_ERR_BAD_CODE, "bit index out of range");
-            bdeg[cidx[k]]++;
-        }
+    if (!n_tasks_out) return set_error(QKD_ERR_INVALID_ARG, "bad arguments");
+    // (build_code's validation first: the sizes below come from cptr)
+    std::vector<int32_t> bdeg;
+    int32_t max_dc = 0;
+    const qkd_status vs = validate_csr(n, m, cptr, cidx, bdeg, max_dc);
+    if (vs != QKD_OK) return vs;
+    std::vector<int32_t> fill(n, 0), krow(cptr[m]);
     for (int32_t j = 0; j < m; ++j)
         for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k) krow[k] = fill[cidx[k]]++;
     qkdp::WavePlan plan;

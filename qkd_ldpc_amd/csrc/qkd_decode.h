@@ -68,6 +68,12 @@ struct DecodeArgs {
     // kModeKeys
     const uint64_t* alice_w;
     const uint64_t* bob_w;
+    // qkd_qkd_ldpc_batch: the caller's byte keys (F x N, 0/1), packed into
+    // alice_w / bob_w by the frame-syndrome kernel itself (the split path's
+    // byte form) or by pack_kernel first (launch_pack_keys); nullptr when the
+    // keys are packed already (device keygen)
+    const uint8_t* alice_b;
+    const uint8_t* bob_b;
     uint32_t words;
     double log_p;
     // First-iteration message table (kModeKeys): with every channel LLR equal
@@ -552,7 +558,6 @@ __host__ __device__ inline uint32_t encode_slot(uint32_t x, uint32_t S, uint32_t
 //   bits 19-31  (j >> 5) * 4: the byte offset of the check's syndrome word
 // (needs M <= 65536: the split decoder's limit).
 constexpr uint32_t kSegStartShift = 5, kSegWiShift = 11, kSegWordShift = 19;
-constexpr int32_t kMaxChecksSplit = 65536;
 __host__ __device__ inline uint32_t encode_seg(uint32_t j, uint32_t start, uint32_t deg, uint32_t lane, uint32_t dc) {
     const uint32_t p = lane - start;
     const uint32_t wi = dc <= 16 ? (deg - 1) * dc + (p < dc - 1 ? p : dc - 1) : deg - 1;
@@ -570,6 +575,8 @@ DecodeFn pick_split_spec(int mode, int max_dc, bool ckpt, int* dc);
 // decode_split.hip, kModeKeys: the kernels around the split decoder.
 // Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.
 hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream);
+// decode.hip: a.alice_b / a.bob_b -> a.alice_w / a.bob_w (original bit order)
+hipError_t launch_pack_keys(const DecodeArgs& a, hipStream_t stream);
 hipError_t launch_key_match(const DecodeArgs& a, hipStream_t stream);
 
 }  // namespace qkd

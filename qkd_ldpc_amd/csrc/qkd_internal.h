@@ -34,6 +34,9 @@ constexpr int kMaxBitsLds = 20480;
 // The split-store kernels (decode_split.hip): Bob's bits of a thread's
 // bit-phase rounds in one 64-bit register, 64 rounds of kDecodeBlock bits
 constexpr int kMaxBitsSplit = 64 * kDecodeBlock;
+// (the split decoder's encoded segment words hold (j >> 5) * 4 in 13 bits:
+// qkd_decode.h encode_seg)
+constexpr int32_t kMaxChecksSplit = 65536;
 // Parallel key generation: 64 lanes per frame, jump levels log2(64); frames
 // with more flipped positions than this take the serial kernel.
 // keygen_fast_kernel: kKeygenLanes lanes per frame (kKeygenLevels = log2 of

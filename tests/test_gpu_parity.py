@@ -247,6 +247,34 @@ def test_qkd_ldpc_batch_matches_trials(Q, H, golden_vectors):
     assert (r.bits.cpu().numpy()[ok] == a.cpu().numpy()[ok]).all()
 
 
+@pytest.mark.parametrize("form", ["bytes", "pack", "bytes_misaligned"])
+def test_qkd_ldpc_byte_keys_forms(Q, H, golden_vectors, monkeypatch, form):
+    """qkd_qkd_ldpc_batch's byte keys: packed inside frame_syn_sliced_kernel (the
+    default when rows allow 8-byte loads), by pack_kernel first (QKD_SYN_BYTES=0),
+    and from 4- but not 8-byte-aligned arrays (pack_kernel, chosen by the launcher);
+    1000 frames (the last 16-frame group ragged). Decoded words, iterations and flags
+    equal the golden config-2 frames."""
+    monkeypatch.setenv("QKD_SYN_BYTES", "0" if form == "pack" else "1")
+    F = 1000
+    seeds = seeds_dev(Q.make_seeds(777, F))
+    a, b, q = Q.keygen(H, seeds, 0.02)
+    if form == "bytes_misaligned":
+        def shift(x):
+            buf = torch.empty(x.numel() + 4, dtype=torch.uint8, device=x.device)
+            v = buf[4:].view(x.shape)
+            v.copy_(x)
+            assert v.data_ptr() % 8 == 4
+            return v
+        a, b = shift(a), shift(b)
+    r = Q.qkd_ldpc(H, a, b, float(q[0]), 50, 100.0, True, want_bits=True)
+    torch.cuda.synchronize()
+    assert (r.iterations.cpu().numpy() == golden_vectors["c2_iters"][:F]).all()
+    assert (r.syndromes_match.cpu().numpy().astype(bool) == golden_vectors["c2_sp"][:F]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == golden_vectors["c2_ko"][:F]).all()
+    ok = r.keys_match.cpu().numpy().astype(bool)
+    assert (r.bits.cpu().numpy()[ok] == a.cpu().numpy()[ok]).all()
+
+
 def test_workspace_and_streams(Q, H, golden_vectors):
     """Two workspaces on two streams give the same per-frame results."""
     seeds = seeds_dev(Q.make_seeds(777, 1024))
