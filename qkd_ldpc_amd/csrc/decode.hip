@@ -1469,6 +1469,7 @@ static qkd_status ws_free(qkd_workspace* ws) {
     if (ws->zout) (void)hipFree(ws->zout);
     if (ws->low) (void)hipFree(ws->low);
     if (ws->ckpt) (void)hipFree(ws->ckpt);
+    if (ws->win) (void)hipFree(ws->win);
     if (ws->spec_stat_ev) (void)hipEventSynchronize(ws->spec_stat_ev);
     if (ws->spec_stat_host) (void)hipHostFree(ws->spec_stat_host);
     if (ws->spec_stat_ev) (void)hipEventDestroy(ws->spec_stat_ev);
@@ -1719,6 +1720,24 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                     a.ckpt_stride = (uint32_t)slots;
                 }
             }
+            a.win = nullptr;
+            a.win_count = 0;
+            if (spec) {
+                // the in-launch policy's windows (zeroed below with the queue)
+                a.win_shift = kSpecWinShift;
+                a.win_lag = kSpecWinLag;
+                a.win_count = (uint32_t)((a.n_frames + (1u << kSpecWinShift) - 1) >> kSpecWinShift);
+                const size_t need = 2 * (size_t)a.win_count;
+                if (ws->win_words < need) {
+                    if (ws->win) QKD_HIP(hipFree(ws->win));
+                    ws->win = nullptr;
+                    ws->win_words = 0;
+                    if (hipMalloc(&ws->win, need * sizeof(uint32_t)) != hipSuccess)
+                        return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate the policy windows");
+                    ws->win_words = need;
+                }
+                a.win = ws->win;
+            }
             if (rule == kRuleSp64) {
                 s = check_no_static_lds(sfn);
                 if (s != QKD_OK) return s;
@@ -1736,6 +1755,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 QKD_HIP(launch_frame_syn(a, stream));
             } else {
                 QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));
+                if (a.win) QKD_HIP(hipMemsetAsync(a.win, 0, 2 * (size_t)a.win_count * sizeof(uint32_t), stream));
             }
             QKD_HIP(decoder_event(ws, stream));
             hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);

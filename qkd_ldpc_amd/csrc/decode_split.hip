@@ -1016,7 +1016,29 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     // frames from the queue: each frame's successor is claimed when the frame
     // starts (thread 0 keeps it in a register until the frame's end), so the
     // atomic's round trip overlaps the prologue's loads
-    if (tid == 0) ctl[1] = atomicAdd(a.counter, 1u);
+    // the in-launch replay policy for frame fr (SPEC kernels; DecodeArgs::win):
+    // whether window fr / W - win_lag replayed at most a sixth of its frames,
+    // waiting (thread 0, between frames) until that window has completed. A
+    // wait cannot deadlock: every frame of a waited-on window is done, being
+    // decoded, or claimed by a workgroup that waits on a strictly earlier window.
+    auto spec_policy = [&](uint32_t fr) -> uint32_t {
+        if (!SPEC || a.spec_always || fr >= a.n_frames) return 1u;
+        const uint32_t wn = fr >> a.win_shift;
+        if (wn < a.win_lag) return 1u;
+        const uint32_t k = wn - a.win_lag, W = 1u << a.win_shift;
+        // (bounded, ~1 s: a defensive exit, never expected to be reached)
+        for (uint32_t polls = 0;
+             __hip_atomic_load(a.win + a.win_count + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < W; ++polls) {
+            if (polls >= (1u << 24)) return 1u;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        const uint32_t rep = __hip_atomic_load(a.win + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return rep * 6u <= W ? 1u : 0u;     // kSpecReplayMax
+    };
+    if (tid == 0) {
+        ctl[1] = atomicAdd(a.counter, 1u);
+        ctl[6] = spec_policy(ctl[1]);
+    }
     uint32_t next_f = 0;
     for (;;) {
         pc.mark(4);
@@ -1028,10 +1050,8 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
         const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl[1]);   // (uniform to the compiler)
         if (f >= a.n_frames) break;
         if (tid == 0) next_f = atomicAdd(a.counter, 1u);
-        // this launch's replays so far (read now, used for the next frame)
-        uint32_t launch_replays = 0;
-        if (SPEC && tid == 0)
-            launch_replays = __hip_atomic_load(a.replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // this frame's replay events (thread 0; the policy's window count)
+        uint32_t frame_replays = 0;
 
         // ---- prologue. Keys path: the frame's Bob words, in the internal
         //      bit order (frame_syn_kernel permuted them), staged in LDS (the
@@ -1100,7 +1120,10 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
         bool spec = spec0;
         // a frame the policy keeps off the speculation counts as replayed (so
         // the policy, once on, stays on, and the call's count reports it)
-        if (SPEC == 1 && !spec && tid == 0) atomicAdd(a.replay_count, 1u);
+        if (SPEC == 1 && !spec && tid == 0) {
+            atomicAdd(a.replay_count, 1u);
+            frame_replays++;
+        }
         bool done = false;
         uint32_t it = 0;
         // checkpointed speculation: the iteration the saved messages feed, and
@@ -1338,6 +1361,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 if (tid == 0) {
                     atomicAdd(a.replay_count, 1u);
                     atomicAdd(a.spec_replays, 1ull);
+                    frame_replays++;
                 }
                 continue;
             }
@@ -1362,6 +1386,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 if (tid == 0) {
                     atomicAdd(a.replay_count, 1u);
                     atomicAdd(a.spec_replays, 1ull);
+                    frame_replays++;
                 }
             } else if (CKPT && !spec && it >= 2 && it + 1 < a.max_it && unsat < ck_lim) {
                 // (exact round: iteration it - 1 left its b2c in the slots, and
@@ -1410,9 +1435,15 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             a.iters[f] = done ? it + 1 : a.max_it;
             a.sp_ok[f] = done ? 1 : 0;
             ctl[1] = next_f;
-            // speculate on the next frame unless a sixth of the frames
-            // started so far (past the first 64) were replayed (kSpecReplayMax)
-            ctl[6] = (a.spec_always || launch_replays * 6u <= next_f + 64u) ? 1u : 0u;
+            if (SPEC) {
+                // this frame into its window (replay events first, then the
+                // completion that publishes them), then the next frame's policy
+                const uint32_t w = f >> a.win_shift;
+                if (frame_replays)
+                    __hip_atomic_fetch_add(a.win + w, frame_replays, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(a.win + a.win_count + w, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                ctl[6] = spec_policy(next_f);
+            }
         }
         __syncthreads();
     }
@@ -1439,13 +1470,15 @@ constexpr int kSynRow = 8;
 // compares Alice's word by word with no gathers of its own.
 __global__ __launch_bounds__(kSynBlock) void frame_syn_kernel(DeviceCode c, uint64_t* alice_w, uint64_t* bob_w,
                                                               uint32_t words, uint32_t n_frames, uint32_t lsign,
-                                                              uint32_t* synw, uint32_t* counter) {
+                                                              uint32_t* synw, uint32_t* counter, uint32_t* win,
+                                                              uint32_t win_words) {
     // [kSynFrames][2 * words] pairs (Alice's 32-bit word, Bob's 32-bit word):
     // one 8-byte LDS read gives both keys' bit
     extern __shared__ uint2 kw[];
     // the decoder's frame queue and replay count (decode.hip launch_decode:
     // this kernel runs first on the stream, in place of a memset)
     if (blockIdx.x == 0 && threadIdx.x < 2) counter[threadIdx.x] = 0;
+    for (uint32_t i = blockIdx.x * kSynBlock + threadIdx.x; i < win_words; i += gridDim.x * kSynBlock) win[i] = 0;
     const uint32_t w32 = 2 * words;
     const uint32_t f0 = blockIdx.x * kSynFrames;
     const uint32_t nf = min((uint32_t)kSynFrames, n_frames - f0);
@@ -1577,6 +1610,7 @@ __global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCo
                                                                         uint64_t* bob_w, uint32_t words,
                                                                         uint32_t n_frames, uint32_t lsign,
                                                                         uint32_t* synw, uint32_t* counter,
+                                                                        uint32_t* win, uint32_t win_words,
                                                                         const uint8_t* alice_b,
                                                                         const uint8_t* bob_b) {
     extern __shared__ uint32_t T[];
@@ -1584,6 +1618,7 @@ __global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCo
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // (uniform to the compiler)
     constexpr uint32_t NW = kSlicedBlock / 64;
     if (blockIdx.x == 0 && tid < 2) counter[tid] = 0;     // (the decoder's queue, as frame_syn_kernel)
+    for (uint32_t i = blockIdx.x * kSlicedBlock + tid; i < win_words; i += gridDim.x * kSlicedBlock) win[i] = 0;
     const uint32_t f0 = blockIdx.x * kSlicedFrames;
     const uint32_t nf = min((uint32_t)kSlicedFrames, n_frames - f0);
     const uint32_t fr = lane & 15u;
@@ -1739,17 +1774,19 @@ hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
         if (bytes)
             hipLaunchKernelGGL(frame_syn_sliced_kernel<true>, grid, dim3(kSlicedBlock), slds, stream, a.code,
                                const_cast<uint64_t*>(a.alice_w), const_cast<uint64_t*>(a.bob_w), a.words,
-                               a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter, a.alice_b, a.bob_b);
+                               a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter, a.win,
+                               2 * a.win_count, a.alice_b, a.bob_b);
         else
             hipLaunchKernelGGL(frame_syn_sliced_kernel<false>, grid, dim3(kSlicedBlock), slds, stream, a.code,
                                const_cast<uint64_t*>(a.alice_w), const_cast<uint64_t*>(a.bob_w), a.words,
-                               a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter, nullptr, nullptr);
+                               a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter, a.win,
+                               2 * a.win_count, nullptr, nullptr);
         return hipGetLastError();
     }
     const size_t lds = (size_t)kSynFrames * 2 * a.words * sizeof(uint64_t);
     hipLaunchKernelGGL(frame_syn_kernel, dim3((a.n_frames + kSynFrames - 1) / kSynFrames), dim3(kSynBlock), lds,
                        stream, a.code, const_cast<uint64_t*>(a.alice_w), const_cast<uint64_t*>(a.bob_w), a.words,
-                       a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter);
+                       a.n_frames, lsign, const_cast<uint32_t*>(a.synw), a.counter, a.win, 2 * a.win_count);
     return hipGetLastError();
 }
 

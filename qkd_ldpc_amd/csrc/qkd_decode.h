@@ -23,6 +23,11 @@ constexpr double kSpecCkptSwitch = 1.0 / 16.0;
 // Replay fraction above which speculation stops: within a launch for the
 // frames still to start (decode_split.hip), across calls for that QBER and up.
 constexpr double kSpecReplayMax = 1.0 / 6.0;
+// the in-launch policy's frame windows (DecodeArgs::win): 256 frames, decided
+// from the window 4 back (1024 frames earlier: by then it has almost always
+// completed, so a frame rarely waits for it)
+constexpr uint32_t kSpecWinShift = 8;
+constexpr uint32_t kSpecWinLag = 4;
 // decode_keys samples the replay count of a QBER that twice stayed under
 // kSpecCkptSwitch only once every this many calls
 constexpr uint64_t kSpecStatEvery = 64;
@@ -132,8 +137,19 @@ struct DecodeArgs {
     // pass a quarter of the frames started, later frames skip the speculation
     uint32_t* replay_count;
     // QKD_SPEC_POLICY=always (tests): the in-launch replay policy never turns
-    // the speculation off, so the replay count depends on the frames alone
+    // the speculation off
     uint32_t spec_always;
+    // The in-launch replay policy over frame-index windows of 2^win_shift
+    // frames (decode_split.hip spec_policy): win[w] counts window w's replay
+    // events, win[win_count + w] its completed frames (zeroed per launch by the
+    // frame-syndrome kernel, or a memset). Frame f speculates iff window
+    // f / W - win_lag replayed at most a sixth of its frames (windows below
+    // win_lag: always) -- a function of the frames alone, not of the order in
+    // which workgroups finish them.
+    uint32_t* win;
+    uint32_t win_count;
+    uint32_t win_shift;
+    uint32_t win_lag;
     // checkpointed speculation (SPEC 2, high QBER): once an exact iteration
     // leaves at most ckpt_unsat checks unsatisfied, the messages are saved to
     // ckpt (ckpt_stride elements per workgroup) and the iterations continue on

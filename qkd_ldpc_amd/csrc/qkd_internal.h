@@ -163,6 +163,9 @@ struct qkd_workspace {
     // checkpointed speculation: one saved message store per resident workgroup
     double* ckpt = nullptr;
     size_t ckpt_slots = 0;
+    // the speculative kernel's in-launch policy windows (DecodeArgs::win)
+    uint32_t* win = nullptr;
+    size_t win_words = 0;
     // qkd_debug_decoder_timing: while on, HIP events bracket every decoder
     // launch on its stream (pairs recorded, read back on collection)
     bool time_decoder = false;

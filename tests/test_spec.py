@@ -399,12 +399,10 @@ def test_fold_table_equals_per_bit_form(Q, H, fresh_seeds, monkeypatch, q):
     """The speculative kernel's folded first iteration from its per-pattern table
     (fold_table_fill) against the per-bit form (QKD_FOLD_TABLE=0): the same psi
     bounds give the same certified rounds, so outputs AND the count of frames the
-    intervals could not certify agree. (QKD_SPEC_POLICY=always: the in-launch
-    replay policy reads a count other workgroups update, so which frames it
-    keeps off the speculation depends on timing, and the two forms run at
-    different speeds.)"""
+    intervals could not certify agree. (The in-launch replay policy decides
+    over frame-index windows, so which frames it keeps off the speculation does
+    not depend on how fast either form runs.)"""
     seeds = fresh_seeds[:20_000]
-    monkeypatch.setenv("QKD_SPEC_POLICY", "always")
     out = {}
     for tab in ("0", "1"):
         monkeypatch.setenv("QKD_FOLD_TABLE", tab)
@@ -462,3 +460,34 @@ def test_psi_of_exact_pair_equals_scalar(Q):
         out[which] = dy.cpu().numpy().view(np.uint64)
     bad = np.nonzero(out[10] != out[11])[0]
     assert bad.size == 0, (bad[:8], x[bad[:8]])
+
+
+@pytest.mark.parametrize("q", [0.05, 0.08])
+def test_replay_policy_independent_of_scheduling(Q, H, fresh_seeds, monkeypatch, q):
+    """The in-launch replay policy (decode_split.hip spec_policy) decides frame f from
+    window f / 256 - 4 of the frame index, so the frames it keeps off the speculation,
+    and with them the replay count, are the same whatever order the workgroups finish
+    their frames in: a fresh workspace's first (speculative) call at a QBER where the
+    policy turns the speculation off, run at the full grid and at 97 and 160
+    workgroups (other completion orders), gives identical outputs AND replay counts."""
+    seeds = fresh_seeds[:12_000]
+    out = {}
+    for grid in ("0", "97", "160"):
+        if grid == "0":
+            monkeypatch.delenv("QKD_DECODE_GRID", raising=False)
+        else:
+            monkeypatch.setenv("QKD_DECODE_GRID", grid)
+        ws = Q.Workspace(H)
+        alice, bob, qx = Q.keygen(H, seeds, q, 0, workspace=ws)
+        Q.spec_replays(ws, reset=True)
+        r = Q.qkd_ldpc(H, alice, bob, float(qx[0].item()), 50, 100.0, True, want_bits=True, workspace=ws)
+        torch.cuda.synchronize()
+        out[grid] = (r, Q.spec_replays(ws))
+        ws.close()
+    (a, na) = out["0"]
+    assert na > 0
+    for g in ("97", "160"):
+        b, nb = out[g]
+        assert torch.equal(a.iterations, b.iterations) and torch.equal(a.bits, b.bits)
+        assert torch.equal(a.keys_match, b.keys_match)
+        assert na == nb, (q, g, na, nb)
