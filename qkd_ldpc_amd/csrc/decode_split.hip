@@ -722,19 +722,32 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
 #define QKD_FIXED_ROWS 1
 #endif
     const bool fixed_rows = QKD_FIXED_ROWS && DV3 && n_pad <= ms.S && ms.S <= 2 * n_pad;
+    // fx: 0 every row chooses per round (ld_row / st_row); 1 fixed rows, row 1
+    // chooses per round; 2 / 3 fixed rows with row 1 in LDS / global for the
+    // whole batch (run picks them per batch: the wave's rounds of row 1 are in
+    // LDS up to a wave-uniform round and global after it, so most batches need
+    // no branch at all -- a branch per access also waits for every load issued
+    // before it)
+#ifndef QKD_R1_SPLIT
+#define QKD_R1_SPLIT 1
+#endif
     auto ld_k = [&](auto fx, int k, uint32_t iw, uint32_t i) -> double {
         const uint32_t x = (uint32_t)k * n_pad + i;
-        if constexpr (decltype(fx)::value) {
+        if constexpr (decltype(fx)::value >= 1) {
             if (k == 0) return ms.l[x];
             if (k == 2) return BufIo<double>::ld(ms.g, (x - ms.S) * 8u);
+            if constexpr (decltype(fx)::value == 2) return ms.l[x];
+            if constexpr (decltype(fx)::value == 3) return BufIo<double>::ld(ms.g, (x - ms.S) * 8u);
         }
         return ms.ld_row((uint32_t)k * n_pad + iw, x);
     };
     auto st_k = [&](auto fx, int k, uint32_t iw, uint32_t i, double v) {
         const uint32_t x = (uint32_t)k * n_pad + i;
-        if constexpr (decltype(fx)::value) {
+        if constexpr (decltype(fx)::value >= 1) {
             if (k == 0) { ms.l[x] = v; return; }
             if (k == 2) { BufIo<double>::st(ms.g, (x - ms.S) * 8u, v); return; }
+            if constexpr (decltype(fx)::value == 2) { ms.l[x] = v; return; }
+            if constexpr (decltype(fx)::value == 3) { BufIo<double>::st(ms.g, (x - ms.S) * 8u, v); return; }
         }
         ms.st_row((uint32_t)k * n_pad + iw, x, v);
     };
@@ -746,8 +759,10 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
         for (int u = 0; u < kIvChunk; ++u) {
             const int i = tid + (r0 + u) * kDecodeBlock;
             const bool ok = i < cn;
-            bc[u] = ok ? c.bit_code[i] : 0;
-            pat[u] = (FOLD && ftab && ok) ? (uint32_t)c.bit_pat[i] : 0u;
+            // (bit_code and bit_pat are padded to whole rounds, host.cpp
+            // build_code: an unconditional load, no exec-mask branch around it)
+            bc[u] = c.bit_code[i];
+            pat[u] = (FOLD && ftab) ? (uint32_t)c.bit_pat[i] : 0u;
             // (wave-uniform, said so: left to itself loop strength reduction
             // rebuilds it from the per-lane bit index, and every row's LDS /
             // global choice becomes a divergent branch with exec-mask shuffling)
@@ -755,6 +770,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k)
                 v[u][k] = FOLD ? 0.0 : ld_k(fx, k, iw, (uint32_t)i);
+            (void)ok;
         }
     };
     auto batch_compute = [&](auto fx, int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
@@ -869,21 +885,33 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             }
         }
     };
-    using NoFx = std::integral_constant<bool, false>;
-    using Fx = std::integral_constant<bool, true>;
-    auto run = [&](auto fx) {
-        for (int r0 = 0; __builtin_amdgcn_readfirstlane(r0 * kDecodeBlock) < cn; r0 += kIvChunk) {
-            VB v;
-            uint64_t bc[kIvChunk];                 // the bits' packed words (DeviceCode::bit_code)
-            uint32_t pat[kIvChunk];                // FOLD with ftab: the bits' degree patterns
-            batch_load(fx, r0, v, bc, pat);
-            batch_compute(fx, r0, v, bc, pat);
-        }
+    using NoFx = std::integral_constant<int, 0>;
+    using Fx = std::integral_constant<int, 1>;
+    using FxL = std::integral_constant<int, 2>;
+    using FxG = std::integral_constant<int, 3>;
+    auto batch = [&](auto fx, int r0) {
+        VB v;
+        uint64_t bc[kIvChunk];                 // the bits' packed words (DeviceCode::bit_code)
+        uint32_t pat[kIvChunk];                // FOLD with ftab: the bits' degree patterns
+        batch_load(fx, r0, v, bc, pat);
+        batch_compute(fx, r0, v, bc, pat);
     };
-    if (fixed_rows)
-        run(Fx{});
-    else
-        run(NoFx{});
+    if (fixed_rows) {
+        for (int r0 = 0; __builtin_amdgcn_readfirstlane(r0 * kDecodeBlock) < cn; r0 += kIvChunk) {
+            // row 1 of the batch's first / last round (wave-uniform; S and
+            // n_pad are multiples of 64, so a wave's 64 slots are one kind)
+            const uint32_t x0 = n_pad + __builtin_amdgcn_readfirstlane((uint32_t)(r0 * kDecodeBlock + wave * 64));
+            const uint32_t x1 = x0 + (uint32_t)(kIvChunk - 1) * kDecodeBlock;
+            if (QKD_R1_SPLIT && x1 < ms.S)
+                batch(FxL{}, r0);
+            else if (QKD_R1_SPLIT && x0 >= ms.S)
+                batch(FxG{}, r0);
+            else
+                batch(Fx{}, r0);
+        }
+    } else {
+        for (int r0 = 0; __builtin_amdgcn_readfirstlane(r0 * kDecodeBlock) < cn; r0 += kIvChunk) batch(NoFx{}, r0);
+    }
 }
 
 // The workgroup's global slot region. QKD_XCD_REGIONS (default): the regions

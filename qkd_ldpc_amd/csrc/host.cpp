@@ -378,7 +378,7 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     QKD_HIP(hipMalloc(&c->d_bit_deg_s, bit_deg_s.size()));
     QKD_HIP(hipMemcpy(c->d_bit_deg_s, bit_deg_s.data(), bit_deg_s.size(), hipMemcpyHostToDevice));
     if (c->n_pat > 0) {
-        std::vector<uint16_t> bit_pat_s(n);
+        std::vector<uint16_t> bit_pat_s(std::max((size_t)n, (size_t)round_up(n, kDecodeBlock)), 0);
         for (int32_t q = 0; q < n; ++q) bit_pat_s[q] = bit_pat[perm[q]];
         QKD_HIP(hipMalloc(&c->d_bit_pat_s, bit_pat_s.size() * sizeof(uint16_t)));
         QKD_HIP(hipMemcpy(c->d_bit_pat_s, bit_pat_s.data(), bit_pat_s.size() * sizeof(uint16_t),
@@ -388,8 +388,11 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     // split kernels only: in the internal order
     bool packable = m <= 65536 && max_dv <= 3;
     for (int32_t j = 0; j < m && packable; ++j) packable = chk_deg[j] >= 1 && chk_deg[j] <= 16;
+    // (both padded with zeros to whole kDecodeBlock rounds: the speculative bit
+    // phase loads them unconditionally, decode_split.hip spec_bit_phase)
+    const size_t rounds_pad = std::max((size_t)c->n_pad, (size_t)round_up(n, kDecodeBlock));
     if (packable) {
-        std::vector<uint64_t> code((size_t)c->n_pad, 0);
+        std::vector<uint64_t> code(rounds_pad, 0);
         for (int32_t q = 0; q < n; ++q) {
             const int32_t i = perm[q];
             uint64_t w = (uint64_t)bdeg[i] << 48;
