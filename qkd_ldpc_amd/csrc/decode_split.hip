@@ -39,6 +39,16 @@
 
 namespace qkd {
 
+// The syndrome test by checks (QKD_SYN_GATHER): the bit phases write their
+// hard decisions (and, speculating, the uncertain ones) as packed words only,
+// and the test gathers each check's parity from them through its row of
+// internal bit numbers (DeviceCode::chk_rows16i); otherwise the bit phases
+// XOR each 1 decision into its checks' syndrome words (LDS atomics).
+#ifndef QKD_SYN_GATHER
+#define QKD_SYN_GATHER 0
+#endif
+constexpr bool kSynGather = QKD_SYN_GATHER != 0;
+
 // The weight of row entry k in the extrinsic sum of a lane at position p
 // (= lane - start) of a segment of degree deg (qkd_decode.h seg_weight_entries).
 template <int DC>
@@ -421,7 +431,7 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
             const bool z = ok && acc <= 0.0f;
             const uint64_t zb = __ballot(z);
             if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
-            if (z) {
+            if (!kSynGather && z) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
                     if (k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
@@ -863,16 +873,26 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 }
             }
             const uint64_t zb = __ballot(z);
-            if (lane == 0 && r * kDecodeBlock + wave * 64 < cn) zw[(r * kDecodeBlock >> 6) + wave] = zb;
-            if (z) {
+            if constexpr (kSynGather) {
+                // decisions and uncertain decisions as packed words (the
+                // syndrome test gathers them by check)
+                const uint64_t ub = __ballot(unc);
+                if (lane == 0 && r * kDecodeBlock + wave * 64 < cn) {
+                    zw[(r * kDecodeBlock >> 6) + wave] = zb;
+                    reinterpret_cast<uint64_t*>(xsyn)[(r * kDecodeBlock >> 6) + wave] = ub;
+                }
+            } else {
+                if (lane == 0 && r * kDecodeBlock + wave * 64 < cn) zw[(r * kDecodeBlock >> 6) + wave] = zb;
+                if (z) {
 #pragma unroll
-                for (int k = 0; k < kDvUnroll; ++k)
-                    if (DV3 || k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
-            }
-            if (unc) {
+                    for (int k = 0; k < kDvUnroll; ++k)
+                        if (DV3 || k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
+                }
+                if (unc) {
 #pragma unroll
-                for (int k = 0; k < kDvUnroll; ++k)
-                    if (DV3 || k < deg) atomicOr(&xunc[jc[k] >> 5], 1u << (jc[k] & 31));
+                    for (int k = 0; k < kDvUnroll; ++k)
+                        if (DV3 || k < deg) atomicOr(&xunc[jc[k] >> 5], 1u << (jc[k] & 31));
+                }
             }
             if (!keep) continue;
             if (DV3 && full) {
@@ -1070,10 +1090,11 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     uint32_t next_f = 0;
     for (;;) {
         pc.mark(4);
-        for (int w = tid; w < m_words; w += kDecodeBlock) {
-            xsyn[w] = 0;
-            xunc[w] = 0;
-        }
+        if (!kSynGather)
+            for (int w = tid; w < m_words; w += kDecodeBlock) {
+                xsyn[w] = 0;
+                xunc[w] = 0;
+            }
         __syncthreads();
         const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl[1]);   // (uniform to the compiler)
         if (f >= a.n_frames) break;
@@ -1292,7 +1313,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                     const bool z = ok && acc <= 0;
                     const uint64_t zb = __ballot(z);
                     if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
-                    if (z) {
+                    if (!kSynGather && z) {
 #pragma unroll
                         for (int k = 0; k < kDvUnroll; ++k)
                             if (k < deg) atomicXor(&xsyn[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
@@ -1346,14 +1367,59 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             // syndrome test (:285): any word differing from the target
             bool mismatch = false, uncertain = false;
             uint32_t nbad = 0;      // checkpointed speculation: unsatisfied checks
-            for (int w = tid; w < m_words; w += kDecodeBlock) {
-                const uint32_t u = xunc[w];
-                const uint32_t d = (xsyn[w] ^ tsyn[w]) & ~u;
-                mismatch |= d != 0;
-                if (CKPT) nbad += __builtin_popcount(d);
-                uncertain |= u != 0;
-                xsyn[w] = 0;
-                xunc[w] = 0;
+            if constexpr (kSynGather) {
+                // each check's parity over its bits' packed decisions (and, in a
+                // speculative round, whether any of them is uncertain), its rows
+                // of internal bit numbers loaded kSynG checks per thread at a time
+                constexpr int kSynG = 4;
+                const uint32_t* zw32 = reinterpret_cast<const uint32_t*>(zw);
+                const uint32_t* uw32 = reinterpret_cast<const uint32_t*>(xsyn);
+                const int rs = c.chk_rs;
+                for (int j0 = 0; j0 < c.m; j0 += kSynG * kDecodeBlock) {
+                    uint4 rw[kSynG][2];
+#pragma unroll
+                    for (int g = 0; g < kSynG; ++g) {
+                        const int j = j0 + g * kDecodeBlock + tid;
+                        const uint4* rp = reinterpret_cast<const uint4*>(c.chk_rows16i + (size_t)(j < c.m ? j : 0) * rs);
+                        rw[g][0] = rp[0];
+                        rw[g][1] = DC > 8 ? rp[1] : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+                    }
+#pragma unroll
+                    for (int g = 0; g < kSynG; ++g) {
+                        const int j = j0 + g * kDecodeBlock + tid;
+                        uint32_t par = 0, un = 0;
+#pragma unroll
+                        for (int h = 0; h < (DC > 8 ? 2 : 1); ++h) {
+                            const uint32_t e2[4] = {rw[g][h].x, rw[g][h].y, rw[g][h].z, rw[g][h].w};
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) {
+                                const uint32_t e = (e2[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                                const bool ok = e != 0xffffu;
+                                const uint32_t q = ok ? e : 0u;
+                                par ^= ok ? (zw32[q >> 5] >> (q & 31u)) : 0u;
+                                if (spec) un |= ok ? (uw32[q >> 5] >> (q & 31u)) : 0u;
+                            }
+                        }
+                        if (j < c.m) {
+                            const uint32_t t = (tsyn[j >> 5] >> (j & 31)) & 1u;
+                            const bool u = (un & 1u) != 0;
+                            const bool bad = ((par ^ t) & 1u) != 0 && !u;
+                            mismatch |= bad;
+                            uncertain |= u;
+                            if (CKPT) nbad += bad ? 1u : 0u;
+                        }
+                    }
+                }
+            } else {
+                for (int w = tid; w < m_words; w += kDecodeBlock) {
+                    const uint32_t u = xunc[w];
+                    const uint32_t d = (xsyn[w] ^ tsyn[w]) & ~u;
+                    mismatch |= d != 0;
+                    if (CKPT) nbad += __builtin_popcount(d);
+                    uncertain |= u != 0;
+                    xsyn[w] = 0;
+                    xunc[w] = 0;
+                }
             }
             const uint32_t wv = __builtin_amdgcn_readfirstlane(
                 (uint32_t)(__any(mismatch) ? 1u : 0u) | (uint32_t)(__any(uncertain) ? 4u : 0u));

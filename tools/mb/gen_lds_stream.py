@@ -26,10 +26,9 @@ def split_lds(n_pad, n_words, m, max_dv, dc, tab2_entries, ftab_entries, esz, bu
     m_words = ((m + 63) // 64) * 2
     a16 = lambda x: (x + 15) & ~15
     tsyn = 0
-    xsyn = tsyn + m_words * 4
-    qsyn = xsyn + m_words * 4
-    xunc = qsyn + m_words * 4
-    zw = a16(xunc + m_words * 4)
+    qsyn = tsyn + m_words * 4
+    xsyn = qsyn + m_words * 4
+    zw = a16(xsyn + max(m_words * 8, (n_pad // 64) * 8))
     tval = a16(zw + (n_pad // 64) * 8)
     rows = 16 * (64 + dc) * esz
     stage = n_words * 16
