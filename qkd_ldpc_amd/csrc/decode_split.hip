@@ -783,15 +783,19 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             (void)ok;
         }
     };
-    auto batch_compute = [&](auto fx, int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
+    // fullc: every round of the batch is full (compile time: no per-round
+    // bounds tests at all)
+    auto batch_compute = [&](auto fx, auto fullc, int r0, VB& v, uint64_t (&bc)[kIvChunk],
+                             uint32_t (&pat)[kIvChunk]) {
+        constexpr bool FULLC = decltype(fullc)::value;
 #pragma unroll
         for (int u = 0; u < kIvChunk; ++u) {
             const int r = r0 + u;
-            if (r * kDecodeBlock >= cn) break;            // block-uniform
+            if (!FULLC && r * kDecodeBlock >= cn) break;            // block-uniform
             const int i = tid + r * kDecodeBlock;
             const uint32_t iw = __builtin_amdgcn_readfirstlane((uint32_t)(r * kDecodeBlock + wave * 64));
             // a full round (block-uniform): every lane's bit exists
-            const bool full = (r + 1) * kDecodeBlock <= cn;
+            const bool full = FULLC || (r + 1) * kDecodeBlock <= cn;
             const bool ok = full || i < cn;
             const int deg = DV3 ? kDvUnroll : (int)(bc[u] >> 48) & 3;
             int32_t jc[kDvUnroll];
@@ -873,16 +877,17 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 }
             }
             const uint64_t zb = __ballot(z);
+            const bool wave_in = FULLC || r * kDecodeBlock + wave * 64 < cn;
             if constexpr (kSynGather) {
                 // decisions and uncertain decisions as packed words (the
                 // syndrome test gathers them by check)
                 const uint64_t ub = __ballot(unc);
-                if (lane == 0 && r * kDecodeBlock + wave * 64 < cn) {
+                if (lane == 0 && wave_in) {
                     zw[(r * kDecodeBlock >> 6) + wave] = zb;
                     reinterpret_cast<uint64_t*>(xsyn)[(r * kDecodeBlock >> 6) + wave] = ub;
                 }
             } else {
-                if (lane == 0 && r * kDecodeBlock + wave * 64 < cn) zw[(r * kDecodeBlock >> 6) + wave] = zb;
+                if (lane == 0 && wave_in) zw[(r * kDecodeBlock >> 6) + wave] = zb;
                 if (z) {
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k)
@@ -909,12 +914,14 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
     using Fx = std::integral_constant<int, 1>;
     using FxL = std::integral_constant<int, 2>;
     using FxG = std::integral_constant<int, 3>;
-    auto batch = [&](auto fx, int r0) {
+    using Full = std::integral_constant<bool, true>;
+    using Part = std::integral_constant<bool, false>;
+    auto batch = [&](auto fx, auto fullc, int r0) {
         VB v;
         uint64_t bc[kIvChunk];                 // the bits' packed words (DeviceCode::bit_code)
         uint32_t pat[kIvChunk];                // FOLD with ftab: the bits' degree patterns
         batch_load(fx, r0, v, bc, pat);
-        batch_compute(fx, r0, v, bc, pat);
+        batch_compute(fx, fullc, r0, v, bc, pat);
     };
     if (fixed_rows) {
         for (int r0 = 0; __builtin_amdgcn_readfirstlane(r0 * kDecodeBlock) < cn; r0 += kIvChunk) {
@@ -922,15 +929,18 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             // n_pad are multiples of 64, so a wave's 64 slots are one kind)
             const uint32_t x0 = n_pad + __builtin_amdgcn_readfirstlane((uint32_t)(r0 * kDecodeBlock + wave * 64));
             const uint32_t x1 = x0 + (uint32_t)(kIvChunk - 1) * kDecodeBlock;
-            if (QKD_R1_SPLIT && x1 < ms.S)
-                batch(FxL{}, r0);
-            else if (QKD_R1_SPLIT && x0 >= ms.S)
-                batch(FxG{}, r0);
+            // (whole batches of full rounds: every bit of every round exists)
+            const bool full = (r0 + kIvChunk) * kDecodeBlock <= cn;
+            if (QKD_R1_SPLIT && full && x1 < ms.S)
+                batch(FxL{}, Full{}, r0);
+            else if (QKD_R1_SPLIT && full && x0 >= ms.S)
+                batch(FxG{}, Full{}, r0);
             else
-                batch(Fx{}, r0);
+                batch(Fx{}, Part{}, r0);
         }
     } else {
-        for (int r0 = 0; __builtin_amdgcn_readfirstlane(r0 * kDecodeBlock) < cn; r0 += kIvChunk) batch(NoFx{}, r0);
+        for (int r0 = 0; __builtin_amdgcn_readfirstlane(r0 * kDecodeBlock) < cn; r0 += kIvChunk)
+            batch(NoFx{}, Part{}, r0);
     }
 }
 

@@ -12,6 +12,8 @@ export TMPDIR=/tmp
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 timeout -k 10 60 rocprofv3 -L > $O/counters_list.txt 2>&1 || echo "counter list rc=$?"
+timeout -k 10 120 ./tools/mb/issue_mb > $O/issue_mb.txt 2>&1 || { cat $O/issue_mb.txt; exit 1; }
+grep "waves/SIMD  4.0" $O/issue_mb.txt
 timeout -k 10 60 ./tools/mb/lds_bank_mb tools/mb/lds_stream.bin > $O/lds_mb.txt 2>&1 || { cat $O/lds_mb.txt; exit 1; }
 cat $O/lds_mb.txt
 timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES --output-format csv -d $O/lds_pmc -o run -- ./tools/mb/lds_bank_mb tools/mb/lds_stream.bin > $O/lds_pmc.log 2>&1 || { tail $O/lds_pmc.log; exit 1; }

@@ -32,6 +32,18 @@ __global__ __launch_bounds__(1024) void k(float* out, unsigned long long* cyc, i
             if constexpr (OP == 4) asm volatile("v_add_f64 %0, %1, %0" : "+v"(d[u]) : "v"(d[0]));
             if constexpr (OP == 5) asm volatile("v_exp_f32 %0, %0" : "+v"(x[u]));
             if constexpr (OP == 6) asm volatile("v_add_f32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 7) asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(y[u]) : "v"(y[0]));
+            if constexpr (OP == 8) asm volatile("v_pk_add_f32 %0, %1, %0" : "+v"(y[u]) : "v"(y[0]));
+            if constexpr (OP == 9) asm volatile("v_log_f32 %0, %0" : "+v"(x[u]));
+            if constexpr (OP == 10) asm volatile("v_rcp_f32 %0, %0" : "+v"(x[u]));
+            if constexpr (OP == 11) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 12) asm volatile("v_add_u32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 13) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(x[u]) : "v"(a), "v"(b));
+            if constexpr (OP == 14) asm volatile("v_bfe_u32 %0, %0, 3, 7" : "+v"(x[u]));
+            if constexpr (OP == 15) asm volatile("v_mov_b32 %0, %1" : "=v"(x[u]) : "v"(x[(u + 1) % ILP]));
+            if constexpr (OP == 16) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 17) asm volatile("v_cmp_gt_f32 vcc, %0, %1" : : "v"(x[u]), "v"(a) : "vcc");
+            if constexpr (OP == 18) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
         }
     }
     __syncthreads();
@@ -79,6 +91,18 @@ int main() {
         run<4, 8>("v_add_f64", d, dc, cus, c[0], c[1]);
         run<5, 8>("v_exp_f32", d, dc, cus, c[0], c[1]);
         run<6, 8>("v_add_f32", d, dc, cus, c[0], c[1]);
+        run<7, 8>("v_pk_mul_f32", d, dc, cus, c[0], c[1]);
+        run<8, 8>("v_pk_add_f32", d, dc, cus, c[0], c[1]);
+        run<9, 8>("v_log_f32", d, dc, cus, c[0], c[1]);
+        run<10, 8>("v_rcp_f32", d, dc, cus, c[0], c[1]);
+        run<11, 8>("v_cndmask_b32", d, dc, cus, c[0], c[1]);
+        run<12, 8>("v_add_u32", d, dc, cus, c[0], c[1]);
+        run<13, 8>("v_med3_f32", d, dc, cus, c[0], c[1]);
+        run<14, 8>("v_bfe_u32", d, dc, cus, c[0], c[1]);
+        run<15, 8>("v_mov_b32", d, dc, cus, c[0], c[1]);
+        run<16, 8>("v_mul_f32", d, dc, cus, c[0], c[1]);
+        run<17, 8>("v_cmp_gt_f32", d, dc, cus, c[0], c[1]);
+        run<18, 8>("v_xor_b32", d, dc, cus, c[0], c[1]);
     }
     return 0;
 }
