@@ -1627,14 +1627,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     // kernel's store.
     const char* kern = getenv("QKD_DECODE_KERNEL");
     const bool classic = kern && !strcmp(kern, "classic");
-#if QKD_SYN_GATHER
-    // (the gathered syndrome test reads the internal-order check rows)
-    const bool split_rows = c->d_chk_rows16i != nullptr;
-#else
-    const bool split_rows = true;
-#endif
     if ((rule == kRuleSp64 || rule == kRuleSp32) && !classic && !a.trace && c->n <= kMaxBitsSplit &&
-        c->m <= kMaxChecksSplit && split_rows) {
+        c->m <= kMaxChecksSplit) {
         int sdc = 0;
         DecodeFn sfn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &sdc);
         const int esz = rule == kRuleSp64 ? 8 : 4;

@@ -39,15 +39,18 @@
 
 namespace qkd {
 
-// The syndrome test by checks (QKD_SYN_GATHER): the bit phases write their
-// hard decisions (and, speculating, the uncertain ones) as packed words only,
-// and the test gathers each check's parity from them through its row of
-// internal bit numbers (DeviceCode::chk_rows16i); otherwise the bit phases
-// XOR each 1 decision into its checks' syndrome words (LDS atomics).
-#ifndef QKD_SYN_GATHER
-#define QKD_SYN_GATHER 0
+// Running syndrome (QKD_RUN_SYN): xsyn holds H * (the current hard
+// decision) across iterations -- initialised per frame to H * bob (keys path;
+// from frame_syn's words) or 0 (LLR path, decision words 0) -- and each bit
+// phase XORs into it only the decisions that changed against the packed
+// words of the last one (zw), instead of every 1 decision into a zeroed xsyn:
+// at QBER 0.02 a few percent of the bits change per iteration, where about
+// half of them are 1, and the LDS atomics run ~8-way bank-conflicted
+// (tools/mb/lds_bank_mb.hip).
+#ifndef QKD_RUN_SYN
+#define QKD_RUN_SYN 0
 #endif
-constexpr bool kSynGather = QKD_SYN_GATHER != 0;
+constexpr bool kRunSyn = QKD_RUN_SYN != 0;
 
 // The weight of row entry k in the extrinsic sum of a lane at position p
 // (= lane - start) of a segment of degree deg (qkd_decode.h seg_weight_entries).
@@ -430,8 +433,9 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
             for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
             const bool z = ok && acc <= 0.0f;
             const uint64_t zb = __ballot(z);
+            const bool flip = kRunSyn ? (z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
             if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
-            if (!kSynGather && z) {
+            if (flip) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
                     if (k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
@@ -878,26 +882,20 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             }
             const uint64_t zb = __ballot(z);
             const bool wave_in = FULLC || r * kDecodeBlock + wave * 64 < cn;
-            if constexpr (kSynGather) {
-                // decisions and uncertain decisions as packed words (the
-                // syndrome test gathers them by check)
-                const uint64_t ub = __ballot(unc);
-                if (lane == 0 && wave_in) {
-                    zw[(r * kDecodeBlock >> 6) + wave] = zb;
-                    reinterpret_cast<uint64_t*>(xsyn)[(r * kDecodeBlock >> 6) + wave] = ub;
-                }
-            } else {
-                if (lane == 0 && wave_in) zw[(r * kDecodeBlock >> 6) + wave] = zb;
-                if (z) {
+            // (running syndrome: the decisions that changed; this round's word
+            // of the last decision is read before lane 0 overwrites it: one
+            // wave's LDS accesses complete in order)
+            const bool flip = kRunSyn ? (z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
+            if (lane == 0 && wave_in) zw[(r * kDecodeBlock >> 6) + wave] = zb;
+            if (flip) {
 #pragma unroll
-                    for (int k = 0; k < kDvUnroll; ++k)
-                        if (DV3 || k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
-                }
-                if (unc) {
+                for (int k = 0; k < kDvUnroll; ++k)
+                    if (DV3 || k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
+            }
+            if (unc) {
 #pragma unroll
-                    for (int k = 0; k < kDvUnroll; ++k)
-                        if (DV3 || k < deg) atomicOr(&xunc[jc[k] >> 5], 1u << (jc[k] & 31));
-                }
+                for (int k = 0; k < kDvUnroll; ++k)
+                    if (DV3 || k < deg) atomicOr(&xunc[jc[k] >> 5], 1u << (jc[k] & 31));
             }
             if (!keep) continue;
             if (DV3 && full) {
@@ -1100,11 +1098,10 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     uint32_t next_f = 0;
     for (;;) {
         pc.mark(4);
-        if (!kSynGather)
-            for (int w = tid; w < m_words; w += kDecodeBlock) {
-                xsyn[w] = 0;
-                xunc[w] = 0;
-            }
+        for (int w = tid; w < m_words; w += kDecodeBlock) {
+            xsyn[w] = 0;
+            xunc[w] = 0;
+        }
         __syncthreads();
         const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl[1]);   // (uniform to the compiler)
         if (f >= a.n_frames) break;
@@ -1159,6 +1156,25 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             if (tid == 0) ms.st((uint32_t)c.n, (T)0);
         };
         init_slots(spec0);
+        // running syndrome (kRunSyn): the last decision = Bob's key (keys path,
+        // the words staged above) or 0 (LLR path), and xsyn = H * it: from
+        // frame_syn's words, q_j = s_j ^ (H bob)_j ^ (deg_j & sign(log_p))
+        if constexpr (kRunSyn) {
+            const int zwords = (int)(n_pad >> 6);
+            for (int q = tid; q < zwords; q += kDecodeBlock)
+                zw[q] = (MODE == kModeKeys && q < (int)a.words) ? bw[q] : 0ull;
+            if (MODE == kModeKeys) {
+                for (int w = tid; w < m_words; w += kDecodeBlock) {
+                    uint32_t odd = 0;
+                    if (lsign)
+                        for (int b = 0; b < 32; ++b) {
+                            const int j = w * 32 + b;
+                            odd |= (j < c.m ? (uint32_t)(c.chk_deg[j] & 1u) : 0u) << b;
+                        }
+                    xsyn[w] = tsyn[w] ^ qsyn[w] ^ odd;
+                }
+            }
+        }
         // ---- prologue, LLR path: target syndrome bits per check (tsyn), thread per check
         if (MODE == kModeLlr) {
             for (int j0 = wave * 64; j0 < c.m; j0 += kDecodeBlock) {
@@ -1322,8 +1338,10 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                     // hard decision z_i = total_i <= 0 (NaN -> 0), one ballot word per wave
                     const bool z = ok && acc <= 0;
                     const uint64_t zb = __ballot(z);
+                    const bool flip =
+                        kRunSyn ? (z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
                     if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
-                    if (!kSynGather && z) {
+                    if (flip) {
 #pragma unroll
                         for (int k = 0; k < kDvUnroll; ++k)
                             if (k < deg) atomicXor(&xsyn[jc[u][k] >> 5], 1u << (jc[u][k] & 31));
@@ -1377,59 +1395,14 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             // syndrome test (:285): any word differing from the target
             bool mismatch = false, uncertain = false;
             uint32_t nbad = 0;      // checkpointed speculation: unsatisfied checks
-            if constexpr (kSynGather) {
-                // each check's parity over its bits' packed decisions (and, in a
-                // speculative round, whether any of them is uncertain), its rows
-                // of internal bit numbers loaded kSynG checks per thread at a time
-                constexpr int kSynG = 4;
-                const uint32_t* zw32 = reinterpret_cast<const uint32_t*>(zw);
-                const uint32_t* uw32 = reinterpret_cast<const uint32_t*>(xsyn);
-                const int rs = c.chk_rs;
-                for (int j0 = 0; j0 < c.m; j0 += kSynG * kDecodeBlock) {
-                    uint4 rw[kSynG][2];
-#pragma unroll
-                    for (int g = 0; g < kSynG; ++g) {
-                        const int j = j0 + g * kDecodeBlock + tid;
-                        const uint4* rp = reinterpret_cast<const uint4*>(c.chk_rows16i + (size_t)(j < c.m ? j : 0) * rs);
-                        rw[g][0] = rp[0];
-                        rw[g][1] = DC > 8 ? rp[1] : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-                    }
-#pragma unroll
-                    for (int g = 0; g < kSynG; ++g) {
-                        const int j = j0 + g * kDecodeBlock + tid;
-                        uint32_t par = 0, un = 0;
-#pragma unroll
-                        for (int h = 0; h < (DC > 8 ? 2 : 1); ++h) {
-                            const uint32_t e2[4] = {rw[g][h].x, rw[g][h].y, rw[g][h].z, rw[g][h].w};
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) {
-                                const uint32_t e = (e2[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-                                const bool ok = e != 0xffffu;
-                                const uint32_t q = ok ? e : 0u;
-                                par ^= ok ? (zw32[q >> 5] >> (q & 31u)) : 0u;
-                                if (spec) un |= ok ? (uw32[q >> 5] >> (q & 31u)) : 0u;
-                            }
-                        }
-                        if (j < c.m) {
-                            const uint32_t t = (tsyn[j >> 5] >> (j & 31)) & 1u;
-                            const bool u = (un & 1u) != 0;
-                            const bool bad = ((par ^ t) & 1u) != 0 && !u;
-                            mismatch |= bad;
-                            uncertain |= u;
-                            if (CKPT) nbad += bad ? 1u : 0u;
-                        }
-                    }
-                }
-            } else {
-                for (int w = tid; w < m_words; w += kDecodeBlock) {
-                    const uint32_t u = xunc[w];
-                    const uint32_t d = (xsyn[w] ^ tsyn[w]) & ~u;
-                    mismatch |= d != 0;
-                    if (CKPT) nbad += __builtin_popcount(d);
-                    uncertain |= u != 0;
-                    xsyn[w] = 0;
-                    xunc[w] = 0;
-                }
+            for (int w = tid; w < m_words; w += kDecodeBlock) {
+                const uint32_t u = xunc[w];
+                const uint32_t d = (xsyn[w] ^ tsyn[w]) & ~u;
+                mismatch |= d != 0;
+                if (CKPT) nbad += __builtin_popcount(d);
+                uncertain |= u != 0;
+                if (!kRunSyn) xsyn[w] = 0;
+                xunc[w] = 0;
             }
             const uint32_t wv = __builtin_amdgcn_readfirstlane(
                 (uint32_t)(__any(mismatch) ? 1u : 0u) | (uint32_t)(__any(uncertain) ? 4u : 0u));

@@ -47,10 +47,9 @@ static void free_device(qkd_code* c) {
     c->d_bit_code = nullptr;
     if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
     for (void* p : {(void*)c->d_perm, (void*)c->d_inv, (void*)c->d_bit_chk_s, (void*)c->d_bit_deg_s,
-                    (void*)c->d_bit_pat_s, (void*)c->d_chk_rows16, (void*)c->d_chk_rows16i})
+                    (void*)c->d_bit_pat_s, (void*)c->d_chk_rows16})
         if (p) (void)hipFree(p);
     c->d_chk_rows16 = nullptr;
-    c->d_chk_rows16i = nullptr;
     c->chk_rs = 0;
     c->d_perm = c->d_inv = c->d_bit_chk_s = nullptr;
     c->d_bit_deg_s = nullptr;
@@ -373,11 +372,6 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         QKD_HIP(hipMalloc(&c->d_chk_rows16, rows.size() * sizeof(uint16_t)));
         QKD_HIP(hipMemcpy(c->d_chk_rows16, rows.data(), rows.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
         c->chk_rs = rs;
-        // the same in the internal order (the split decoder's syndrome test)
-        for (size_t k = 0; k < rows.size(); ++k)
-            if (rows[k] != 0xffff) rows[k] = (uint16_t)inv[rows[k]];
-        QKD_HIP(hipMalloc(&c->d_chk_rows16i, rows.size() * sizeof(uint16_t)));
-        QKD_HIP(hipMemcpy(c->d_chk_rows16i, rows.data(), rows.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     }
     QKD_HIP(hipMalloc(&c->d_bit_chk_s, bit_chk_s.size() * sizeof(int32_t)));
     QKD_HIP(hipMemcpy(c->d_bit_chk_s, bit_chk_s.data(), bit_chk_s.size() * sizeof(int32_t), hipMemcpyHostToDevice));

@@ -528,13 +528,9 @@ struct SplitLds {
         const int m_words = decode_m_words(m);
         tsyn = 0;
         qsyn = tsyn + (size_t)m_words * 4;
-        // xsyn and xunc adjacent: with the gathered syndrome test
-        // (QKD_SYN_GATHER) the two hold the uncertainty words of the bits
-        // instead (n_pad / 64 uint64), so the region is at least that large
         xsyn = qsyn + (size_t)m_words * 4;
         xunc = xsyn + (size_t)m_words * 4;
-        const size_t xreg = (size_t)m_words * 8 > (size_t)(n_pad / 64) * 8 ? (size_t)m_words * 8 : (size_t)(n_pad / 64) * 8;
-        zw = (xsyn + xreg + 15) & ~(size_t)15;
+        zw = (xunc + (size_t)m_words * 4 + 15) & ~(size_t)15;
         tval = (zw + (size_t)(n_pad / 64) * 8 + 15) & ~(size_t)15;
         const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * esz;
         const size_t stage = (size_t)n_words * 16;

@@ -113,10 +113,6 @@ struct DeviceCode {
     // past the row; chk_rs 8 or 16)
     const uint16_t* chk_rows16;
     int32_t chk_rs;
-    // the same rows with the split kernels' INTERNAL bit numbers (the split
-    // decoder's syndrome test gathers each check's hard decisions from the
-    // packed decision words; nullptr where chk_rows16 is)
-    const uint16_t* chk_rows16i;
 };
 
 }  // namespace qkd
@@ -210,7 +206,6 @@ struct qkd_code {
     int32_t* d_inv = nullptr;
     // frame_syn_sliced_kernel's compact check rows (host.cpp)
     uint16_t* d_chk_rows16 = nullptr;
-    uint16_t* d_chk_rows16i = nullptr;
     int32_t chk_rs = 0;
     int32_t* d_bit_chk_s = nullptr;
     uint8_t* d_bit_deg_s = nullptr;
@@ -236,14 +231,14 @@ struct qkd_code {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
                                n_pat, d_bit_pat, d_pat_deg, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, 0, nullptr};
+                               nullptr, 0};
     }
     // the split kernels' view (internal bit order, DeviceCode::perm)
     qkd::DeviceCode view_split() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk_s, nullptr, d_bit_deg_s,
                                n_pat, d_bit_pat_s, d_pat_deg, d_bit_code, d_plan_slot, d_perm, d_inv,
-                               d_chk_rows16, chk_rs, d_chk_rows16i};
+                               d_chk_rows16, chk_rs};
     }
 };
 

@@ -28,7 +28,7 @@ def split_lds(n_pad, n_words, m, max_dv, dc, tab2_entries, ftab_entries, esz, bu
     tsyn = 0
     qsyn = tsyn + m_words * 4
     xsyn = qsyn + m_words * 4
-    zw = a16(xsyn + max(m_words * 8, (n_pad // 64) * 8))
+    zw = a16(xsyn + m_words * 8)
     tval = a16(zw + (n_pad // 64) * 8)
     rows = 16 * (64 + dc) * esz
     stage = n_words * 16
