@@ -1077,19 +1077,27 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     // waiting (thread 0, between frames) until that window has completed. A
     // wait cannot deadlock: every frame of a waited-on window is done, being
     // decoded, or claimed by a workgroup that waits on a strictly earlier window.
+    // A window is ONE 64-bit word (completed frames in the low half, replay
+    // events in the high half) updated by one relaxed atomic add, so its two
+    // counts are always read together and no release / acquire ordering is
+    // needed: at agent scope those compile to a write-back (buffer_wbl2) and
+    // an invalidation (buffer_inv) of the whole L2, which the frame loop can
+    // not afford (measured +21 % per config-2 batch).
+    unsigned long long* const win64 = reinterpret_cast<unsigned long long*>(a.win);
     auto spec_policy = [&](uint32_t fr) -> uint32_t {
         if (!SPEC || a.spec_always || fr >= a.n_frames) return 1u;
         const uint32_t wn = fr >> a.win_shift;
         if (wn < a.win_lag) return 1u;
         const uint32_t k = wn - a.win_lag, W = 1u << a.win_shift;
+        unsigned long long v = 0;
         // (bounded, ~1 s: a defensive exit, never expected to be reached)
-        for (uint32_t polls = 0;
-             __hip_atomic_load(a.win + a.win_count + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < W; ++polls) {
+        for (uint32_t polls = 0;; ++polls) {
+            v = __hip_atomic_load(win64 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)v >= W) break;
             if (polls >= (1u << 24)) return 1u;
             __builtin_amdgcn_s_sleep(2);
         }
-        const uint32_t rep = __hip_atomic_load(a.win + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return rep * 6u <= W ? 1u : 0u;     // kSpecReplayMax
+        return (uint32_t)(v >> 32) * 6u <= W ? 1u : 0u;     // kSpecReplayMax
     };
     if (tid == 0) {
         ctl[1] = atomicAdd(a.counter, 1u);
@@ -1513,12 +1521,10 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             a.sp_ok[f] = done ? 1 : 0;
             ctl[1] = next_f;
             if (SPEC) {
-                // this frame into its window (replay events first, then the
-                // completion that publishes them), then the next frame's policy
-                const uint32_t w = f >> a.win_shift;
-                if (frame_replays)
-                    __hip_atomic_fetch_add(a.win + w, frame_replays, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_add(a.win + a.win_count + w, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                // this frame into its window (its completion and its replay
+                // events in one add), then the next frame's policy
+                __hip_atomic_fetch_add(win64 + (f >> a.win_shift), ((unsigned long long)frame_replays << 32) | 1ull,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ctl[6] = spec_policy(next_f);
             }
         }

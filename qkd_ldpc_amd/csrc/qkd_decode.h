@@ -140,9 +140,10 @@ struct DecodeArgs {
     // the speculation off
     uint32_t spec_always;
     // The in-launch replay policy over frame-index windows of 2^win_shift
-    // frames (decode_split.hip spec_policy): win[w] counts window w's replay
-    // events, win[win_count + w] its completed frames (zeroed per launch by the
-    // frame-syndrome kernel, or a memset). Frame f speculates iff window
+    // frames (decode_split.hip spec_policy): 64-bit word w of win (2 *
+    // win_count uint32) holds window w's completed frames (low half) and
+    // replay events (high half), zeroed per launch by the frame-syndrome
+    // kernel, or a memset. Frame f speculates iff window
     // f / W - win_lag replayed at most a sixth of its frames (windows below
     // win_lag: always) -- a function of the frames alone, not of the order in
     // which workgroups finish them.
