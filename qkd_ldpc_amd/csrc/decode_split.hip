@@ -48,7 +48,7 @@ namespace qkd {
 // half of them are 1, and the LDS atomics run ~8-way bank-conflicted
 // (tools/mb/lds_bank_mb.hip).
 #ifndef QKD_RUN_SYN
-#define QKD_RUN_SYN 0
+#define QKD_RUN_SYN 1
 #endif
 constexpr bool kRunSyn = QKD_RUN_SYN != 0;
 

@@ -92,7 +92,11 @@ inline bool build_wave_plan(int32_t n, int32_t m, const int32_t* cptr, const int
         for (int i = 0; i < nc; ++i) {
             const int d = degs[i];
             const int avail = (int)(by_deg[d].size() - next[d]);
-            for (int c = 0; c <= cap; ++c) {
+            // (fills c descending: a fill reachable several ways keeps the way
+            // with the most of the larger degrees, the first to reach it --
+            // ascending, N = 10240 packed 4x6 + 8x5 before 9x6 + 2x5 and ran
+            // out of degree-5 checks after 83 tasks: 507 tasks instead of 490)
+            for (int c = cap; c >= 0; --c) {
                 if (!reach[i][c]) continue;
                 // prefer more of the larger degree: highest count first wins the slot
                 for (int x = std::min(avail, (cap - c) / d); x >= 0; --x) {
@@ -132,6 +136,11 @@ inline bool build_wave_plan(int32_t n, int32_t m, const int32_t* cptr, const int
                 lane += d;
             }
         }
+        // idle lanes as degree-1 segments of their own (start = the lane): an
+        // extrinsic-sum read of row[start + k] then stays beside the lane's
+        // neighbours' entries (start 0 put it on the banks of lane 32's and
+        // lane 48's reads: ~5 extra LDS cycles per task, tools/lds_stream_model.py)
+        for (int l = lane; l < 64; ++l) p.seg[(size_t)task * 64 + l] = plan_seg(0, (uint32_t)l, 1);
     }
     p.word.resize((size_t)(p.n_tasks + kPlanPadTasks) * 64, idle);
     p.seg.resize((size_t)(p.n_tasks + kPlanPadTasks) * 64, idle_seg);

@@ -41,7 +41,7 @@ def split_lds(n_pad, n_words, m, max_dv, dc, tab2_entries, ftab_entries, esz, bu
     slots = max_dv * n_pad
     fit = (budget - msg) // esz - 64 if budget > msg + 64 * esz else 0
     S = min(slots, fit) & ~63
-    return dict(xsyn=xsyn, msg=msg, S=S)
+    return dict(xsyn=xsyn, msg=msg, S=S, zw=zw, wtab=wtab)
 
 
 def main():
