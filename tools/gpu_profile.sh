@@ -7,7 +7,7 @@
 # Each step has its own time limit; any failure ends the script.
 set -u
 cd "$(dirname "$0")/.."
-OUT=${OUT:-gpurun_out/r03prof}
+OUT=${OUT:-gpurun_out/r05prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 VARIANTS=${VARIANTS:-"sp_f64 sp_f32 minsum minsum_sc"}
@@ -35,6 +35,8 @@ WRITE_SIZE
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SMEM
 TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT
+SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64
+SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_LDS_ATOMIC SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_INSTS_BRANCH SQ_INST_CYCLES_SALU
 PASSES
   python3 tools/pmc_traffic.py "$OUT/pmc_$v.json" "$OUT/kernel_summary.json" $dirs || exit 5
 done
