@@ -1084,24 +1084,34 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     // an invalidation (buffer_inv) of the whole L2, which the frame loop can
     // not afford (measured +21 % per config-2 batch).
     unsigned long long* const win64 = reinterpret_cast<unsigned long long*>(a.win);
-    auto spec_policy = [&](uint32_t fr) -> uint32_t {
-        if (!SPEC || a.spec_always || fr >= a.n_frames) return 1u;
+    // window_of(fr): the window frame fr's policy reads, or -1 (none: always on)
+    auto window_of = [&](uint32_t fr) -> int {
+        if (!SPEC || a.spec_always || fr >= a.n_frames) return -1;
         const uint32_t wn = fr >> a.win_shift;
-        if (wn < a.win_lag) return 1u;
-        const uint32_t k = wn - a.win_lag, W = 1u << a.win_shift;
-        unsigned long long v = 0;
+        return wn < a.win_lag ? -1 : (int)(wn - a.win_lag);
+    };
+    // v: that window's word as read earlier (the frame's start, so the load's
+    // latency overlaps the frame; almost always complete by then), polled again
+    // only while incomplete
+    auto spec_policy = [&](uint32_t fr, unsigned long long v) -> uint32_t {
+        const int k = window_of(fr);
+        if (k < 0) return 1u;
+        const uint32_t W = 1u << a.win_shift;
         // (bounded, ~1 s: a defensive exit, never expected to be reached)
-        for (uint32_t polls = 0;; ++polls) {
-            v = __hip_atomic_load(win64 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)v >= W) break;
+        for (uint32_t polls = 0; (uint32_t)v < W; ++polls) {
             if (polls >= (1u << 24)) return 1u;
             __builtin_amdgcn_s_sleep(2);
+            v = __hip_atomic_load(win64 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return (uint32_t)(v >> 32) * 6u <= W ? 1u : 0u;     // kSpecReplayMax
     };
+    auto window_peek = [&](uint32_t fr) -> unsigned long long {
+        const int k = window_of(fr);
+        return k < 0 ? 0ull : __hip_atomic_load(win64 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     if (tid == 0) {
         ctl[1] = atomicAdd(a.counter, 1u);
-        ctl[6] = spec_policy(ctl[1]);
+        ctl[6] = spec_policy(ctl[1], window_peek(ctl[1]));
     }
     uint32_t next_f = 0;
     for (;;) {
@@ -1197,6 +1207,11 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
         }
         __syncthreads();
         pc.mark(0);
+        // (thread 0: the next frame's policy window, read here, after the
+        // prologue has waited out next_f's atomic, so the load's latency
+        // overlaps this frame's iterations)
+        unsigned long long next_win = 0;
+        if (SPEC && tid == 0) next_win = window_peek(next_f);
 
         // ---- iterations (:212-330): interval iterations (qkd_spec.h) in the
         //      speculative launch, the reference's binary64 ones otherwise
@@ -1525,7 +1540,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 // events in one add), then the next frame's policy
                 __hip_atomic_fetch_add(win64 + (f >> a.win_shift), ((unsigned long long)frame_replays << 32) | 1ull,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ctl[6] = spec_policy(next_f);
+                ctl[6] = spec_policy(next_f, next_win);
             }
         }
         __syncthreads();
