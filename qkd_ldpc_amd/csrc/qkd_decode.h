@@ -24,10 +24,11 @@ constexpr double kSpecCkptSwitch = 1.0 / 16.0;
 // frames still to start (decode_split.hip), across calls for that QBER and up.
 constexpr double kSpecReplayMax = 1.0 / 6.0;
 // the in-launch policy's frame windows (DecodeArgs::win): 256 frames, decided
-// from the window 4 back (1024 frames earlier: by then it has almost always
-// completed, so a frame rarely waits for it)
+// from the window 8 back (2048 frames earlier, ~8 frame-times at 256 resident
+// workgroups: by then it has almost always completed; with the window 4 back
+// the waits for a window's last slow frames cost 3.5 % per config-2 batch)
 constexpr uint32_t kSpecWinShift = 8;
-constexpr uint32_t kSpecWinLag = 4;
+constexpr uint32_t kSpecWinLag = 8;
 // decode_keys samples the replay count of a QBER that twice stayed under
 // kSpecCkptSwitch only once every this many calls
 constexpr uint64_t kSpecStatEvery = 64;

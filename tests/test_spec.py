@@ -465,7 +465,7 @@ def test_psi_of_exact_pair_equals_scalar(Q):
 @pytest.mark.parametrize("q", [0.05, 0.08])
 def test_replay_policy_independent_of_scheduling(Q, H, fresh_seeds, monkeypatch, q):
     """The in-launch replay policy (decode_split.hip spec_policy) decides frame f from
-    window f / 256 - 4 of the frame index, so the frames it keeps off the speculation,
+    window f / 256 - 8 of the frame index, so the frames it keeps off the speculation,
     and with them the replay count, are the same whatever order the workgroups finish
     their frames in: a fresh workspace's first (speculative) call at a QBER where the
     policy turns the speculation off, run at the full grid and at 97 and 160
