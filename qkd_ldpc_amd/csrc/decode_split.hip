@@ -433,7 +433,8 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
             for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
             const bool z = ok && acc <= 0.0f;
             const uint64_t zb = __ballot(z);
-            const bool flip = kRunSyn ? (z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
+            const bool flip =
+                kRunSyn ? (ok && z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
             if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
             if (flip) {
 #pragma unroll
@@ -885,7 +886,9 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             // (running syndrome: the decisions that changed; this round's word
             // of the last decision is read before lane 0 overwrites it: one
             // wave's LDS accesses complete in order)
-            const bool flip = kRunSyn ? (z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
+            // (lanes past N never flip: their word may lie past zw's end)
+            const bool flip =
+                kRunSyn ? (ok && z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
             if (lane == 0 && wave_in) zw[(r * kDecodeBlock >> 6) + wave] = zb;
             if (flip) {
 #pragma unroll
@@ -1362,7 +1365,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                     const bool z = ok && acc <= 0;
                     const uint64_t zb = __ballot(z);
                     const bool flip =
-                        kRunSyn ? (z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
+                        kRunSyn ? (ok && z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
                     if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
                     if (flip) {
 #pragma unroll
