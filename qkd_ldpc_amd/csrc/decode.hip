@@ -1764,8 +1764,6 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             return QKD_OK;
         }
     }
-    // (byte keys: the classic kernel reads them packed, in the original order)
-    if (mode == kModeKeys && a.alice_b) QKD_HIP(launch_pack_keys(a, stream));
     const bool gt = decode_needs_gt(c, rule, a.tab2_entries);
     if (gt) {                                     // large code: no per-bit LDS tables
         a.first_table = 0;
@@ -1782,6 +1780,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     s = ws_reserve_decode(ws, (rule == kRuleMinSumLds || rule == kRuleMinSumLdsSc) ? 0 : (size_t)grid);   // no global messages
     if (s != QKD_OK) return s;
     a.code = c->view();
+    // (byte keys: the classic kernel reads them packed, in the original order)
+    if (mode == kModeKeys && a.alice_b) QKD_HIP(launch_pack_keys(a, stream));
     a.c2b = ws->c2b;
     a.c2b_stride = (size_t)c->max_dv * c->n_pad;
     // the workspace holds one total row per slot after all the message stores
