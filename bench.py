@@ -149,12 +149,18 @@ def roofline_block(variant, alg_bytes, kernel_s, call_s, kernel_name):
     The decoder is VALU-issue / latency bound, not HBM bound: its
     speculative rounds run binary32 intervals and most message slots sit in LDS, so it
     never moves the reference's two-array binary64 bytes. The headline is therefore
-    the VALU issue fraction from the kernel's PMC record (separate rocprofv3 --pmc
-    passes, tools/pmc_traffic.py), reproducible from that file alone:
-        frac = SQ_INSTS_VALU x 2 cycles / (kernel cycles x 1024 SIMDs)
-    with kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs of the counted dispatches;
-    achieved = SQ_INSTS_VALU / (the counted dispatches' own duration) and peak =
-    1024 SIMDs / 2 cycles x their effective clock, so frac = achieved / peak.
+    the VALU issue fraction of the kernel's PMC record (separate rocprofv3 --pmc
+    passes, tools/pmc_traffic.py), priced by instruction mix and reproducible from
+    that file and profiles/r*_issue_mb.txt alone:
+        frac = sum over VALU classes (SQ_INSTS_VALU_<class> x its 4-wave issue cost)
+               / (kernel cycles x 1024 SIMDs)
+    with kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs of the counted dispatches, the costs
+    measured at this decoder's occupancy (4 waves per SIMD, tools/mb/issue_mb.hip) and
+    the unclassified rest at the mean of the measured move / logic / compare costs;
+    achieved = the needed SIMD-issue cycles per second and peak = 1024 SIMDs x the
+    effective clock, so frac = achieved / peak. frac_2cyc keeps every instruction at
+    2 cycles (SQ_INSTS_VALU x 2 / (kernel cycles x 1024), a lower bound of the issue
+    time). A record without the class counters falls back to frac_2cyc.
     Beside it:
       live              the same instruction count over THIS run's decoder time (HIP
                         events around each launch on its stream), at the PMC pass's
@@ -182,20 +188,36 @@ def roofline_block(variant, alg_bytes, kernel_s, call_s, kernel_name):
         return {"bound": "hbm", "achieved": alg_bytes / kernel_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": nominal, "traffic": None, "nominal": True, **base}
     pmc_s = cyc / (clk * 1e9)                        # the counted dispatches' duration
-    frac = insts * VALU_ISSUE_CYC / (cyc * N_SIMD)
-    peak = N_SIMD / VALU_ISSUE_CYC * clk             # G wave-instructions / s
-    out = {"bound": "valu", "achieved": insts / pmc_s / 1e9, "peak": peak, "unit": "G wave-inst/s",
-           "frac": frac, "traffic": rec.get("hbm_bytes_per_launch"),
-           "formula": "frac = SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE/8 x 1024) of the PMC record",
+    frac_2cyc = insts * VALU_ISSUE_CYC / (cyc * N_SIMD)
+    mix = v.get("mix")
+    if mix:
+        # the kernel's own VALU instruction mix priced at what 4 waves per SIMD
+        # issue (tools/pmc_traffic.py valu_mix): achieved = SIMD-cycles of VALU
+        # issue the launch needs per second, peak = 1024 SIMDs x the clock
+        achieved = mix["simd_cycles_needed"] / pmc_s / 1e9
+        peak = N_SIMD * clk
+        out = {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G SIMD-issue-cycles/s",
+               "frac": mix["frac_mix"], "frac_2cyc": frac_2cyc,
+               "formula": "frac = sum over VALU classes (PMC count x 4-wave issue cost) / (GRBM_GUI_ACTIVE/8 x "
+                          "1024 SIMDs); frac_2cyc = SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE/8 x 1024), every "
+                          "instruction at 2 cycles",
+               "mix": mix}
+    else:
+        out = {"bound": "valu", "achieved": insts / pmc_s / 1e9, "peak": N_SIMD / VALU_ISSUE_CYC * clk,
+               "unit": "G wave-inst/s", "frac": frac_2cyc, "frac_2cyc": frac_2cyc,
+               "formula": "frac = SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE/8 x 1024) of the PMC record"}
+    out.update({"traffic": rec.get("hbm_bytes_per_launch"),
            "pmc_source": src, "pmc_kernel": rec.get("kernel"),
            "valu_insts_per_launch": insts, "pmc_kernel_cycles": cyc, "pmc_clock_ghz": clk,
            "pmc_kernel_ms": pmc_s * 1e3,
            "hbm_frac_measured": rec["hbm_bytes_per_launch"] / pmc_s / 1e9 / HBM_PEAK_GBS,
            "live": {"kernel_ms": kernel_s * 1e3,
                     "frac_at_pmc_clock": insts * VALU_ISSUE_CYC / (kernel_s * clk * 1e9 * N_SIMD),
-                    "frac_at_rated_clock": insts * VALU_ISSUE_CYC / (kernel_s * RATED_CLOCK_GHZ * 1e9 * N_SIMD)},
+                    "frac_at_rated_clock": insts * VALU_ISSUE_CYC / (kernel_s * RATED_CLOCK_GHZ * 1e9 * N_SIMD),
+                    "frac_mix_at_pmc_clock": (mix["simd_cycles_needed"] / (kernel_s * clk * 1e9 * N_SIMD)
+                                              if mix else None)},
            "valu_active_frac": v.get("valu_active_util_x4"), "wait_frac": v.get("wait_frac"),
-           "lds_conflict_frac": v.get("lds_conflict_frac"), **base}
+           "lds_conflict_frac": v.get("lds_conflict_frac"), **base})
     ceil = issue_ceiling_4waves()
     if ceil:
         c = ceil["cycles_per_wave_inst"]

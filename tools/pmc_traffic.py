@@ -34,6 +34,65 @@ def collect(dirs):
     return per, dur
 
 
+# VALU issue cost per wave64 instruction per SIMD at 4 waves per SIMD (the split
+# decoder's occupancy), ILP 8, shader cycles: tools/mb/issue_mb.hip,
+# profiles/r05_issue_mb.txt. Packed binary32 ops count ONCE in the
+# SQ_INSTS_VALU_{FMA,MUL,ADD}_F32 counters (the ISA census of the check-phase
+# loops times their trip counts reproduces FMA_F32 to 2 %), so each class is
+# priced at its packed share (same census) of the packed cost.
+ISSUE_MB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "profiles", "r05_issue_mb.txt")
+
+
+def issue_costs(path=ISSUE_MB, waves=4.0, ilp=8):
+    """{instruction: cycles per wave-instruction per SIMD} at `waves` waves/SIMD and
+    the given ILP, from the committed issue micro-benchmark output."""
+    out = {}
+    for line in open(path):
+        f = line.split()
+        if len(f) == 7 and float(f[2]) == waves and int(f[4]) == ilp:
+            out[f[0]] = float(f[6])
+    return out
+
+
+# packed shares per class (census of the paired and iteration-2 check-phase steps
+# and the speculative bit-phase rounds, weighted by their config-2 trip counts)
+PACKED_SHARE = {"FMA_F32": 0.62, "MUL_F32": 0.45, "ADD_F32": 0.63}
+
+
+def valu_mix(c, cycles):
+    """The VALU instruction mix of the PMC record priced at the 4-wave issue
+    costs: the SIMD-cycles the kernel's VALU stream needs at those rates, and the
+    share of the kernel's SIMD-cycles that is (frac_mix = the issue-bound
+    fraction at the kernel's own instruction mix)."""
+    keys = ["SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_ADD_F32",
+            "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_INT32"]
+    if not all(k in c for k in keys + ["SQ_INSTS_VALU"]) or not cycles:
+        return None
+    I = issue_costs()
+    price = {
+        "FMA_F32": PACKED_SHARE["FMA_F32"] * I["v_pk_fma_f32"] + (1 - PACKED_SHARE["FMA_F32"]) * I["v_fma_f32"],
+        "MUL_F32": PACKED_SHARE["MUL_F32"] * I["v_pk_mul_f32"] + (1 - PACKED_SHARE["MUL_F32"]) * I["v_mul_f32"],
+        "ADD_F32": PACKED_SHARE["ADD_F32"] * I["v_pk_add_f32"] + (1 - PACKED_SHARE["ADD_F32"]) * I["v_add_f32"],
+        "TRANS_F32": (I["v_exp_f32"] + I["v_log_f32"] + I["v_rcp_f32"]) / 3,
+        "F64": I["v_fma_f64"], "TRANS_F64": 2 * I["v_fma_f64"],
+        "INT32": I["v_add_u32"], "INT64": 2 * I["v_add_u32"], "CVT": I["v_add_u32"],
+        # the rest (selects, compares, moves, logic, med3 / max, lane reads): the
+        # mean of the measured v_mov, v_xor, v_bfe, v_med3 and v_cmp costs
+        "OTHER": sum(I[k] for k in ("v_mov_b32", "v_xor_b32", "v_bfe_u32", "v_med3_f32", "v_cmp_gt_f32")) / 5,
+    }
+    g = lambda k: c.get("SQ_INSTS_VALU_" + k, 0.0)
+    n = {"FMA_F32": g("FMA_F32"), "MUL_F32": g("MUL_F32"), "ADD_F32": g("ADD_F32"), "TRANS_F32": g("TRANS_F32"),
+         "F64": g("ADD_F64") + g("MUL_F64") + g("FMA_F64"), "TRANS_F64": g("TRANS_F64"),
+         "INT32": g("INT32"), "INT64": g("INT64"), "CVT": g("CVT")}
+    n["OTHER"] = max(0.0, c["SQ_INSTS_VALU"] - sum(n.values()))
+    need = sum(n[k] * price[k] for k in n)
+    return {"counts": n, "price_cycles_4waves": price, "packed_share": PACKED_SHARE,
+            "issue_source": "tools/mb/issue_mb.hip at 4 waves/SIMD, ILP 8 (profiles/r05_issue_mb.txt)",
+            "simd_cycles_needed": need, "frac_mix": need / (cycles * N_SIMD),
+            "formula": "frac_mix = sum_class(count x price) / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)"}
+
+
 def main():
     out_path, summary, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
     per, dur = collect(dirs)
@@ -71,6 +130,9 @@ def main():
             v["valu_issue_util_2cyc"] = c["SQ_INSTS_VALU"] * 2 / (cyc * N_SIMD)
         if "SQ_ACTIVE_INST_VALU" in c:
             v["valu_active_util_x4"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (cyc * N_SIMD)
+    mix = valu_mix(c, v.get("gpu_cycles"))
+    if mix:
+        v["mix"] = mix
     if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c:
         v["lds_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
     if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
