@@ -33,7 +33,8 @@ def mix_priced_frac(c):
     """Restated independently of tools/pmc_traffic.py: each VALU class of the PMC
     record at its measured 4-wave issue cost (binary32 FMA / MUL / ADD split packed
     vs scalar by the census shares DESIGN.md §4.3 states; the unclassified rest at
-    the mean of v_mov, v_xor, v_bfe, v_med3, v_cmp), over the kernel's SIMD-cycles."""
+    the mean of v_mov, v_xor, v_bfe, v_med3, v_cmp, v_cndmask with an SGPR mask),
+    over the kernel's SIMD-cycles."""
     k = issue_4waves()
     pk = {"FMA": (0.62, "v_pk_fma_f32", "v_fma_f32"), "MUL": (0.45, "v_pk_mul_f32", "v_mul_f32"),
           "ADD": (0.63, "v_pk_add_f32", "v_add_f32")}
@@ -47,7 +48,8 @@ def mix_priced_frac(c):
     need += g("TRANS_F32") * trans + f64 * k["v_fma_f64"] + g("TRANS_F64") * 2 * k["v_fma_f64"]
     need += (g("INT32") + g("CVT")) * k["v_add_u32"] + g("INT64") * 2 * k["v_add_u32"]
     counted += g("TRANS_F32") + f64 + g("TRANS_F64") + g("INT32") + g("CVT") + g("INT64")
-    rest = sum(k[x] for x in ("v_mov_b32", "v_xor_b32", "v_bfe_u32", "v_med3_f32", "v_cmp_gt_f32")) / 5
+    kinds = ("v_mov_b32", "v_xor_b32", "v_bfe_u32", "v_med3_f32", "v_cmp_gt_f32", "v_cndmask_b32_sgpr")
+    rest = sum(k[x] for x in kinds) / len(kinds)
     need += max(0.0, c["SQ_INSTS_VALU"] - counted) * rest
     return need / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
 

@@ -34,6 +34,13 @@ for _ in range(steps):
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t) / steps
 it = r.iterations.cpu().numpy()
+# lockstep model of a frame-interleaved store: g frames decoded
+# together run as long as their slowest; without refill a batch costs the sum
+# over groups of the group maximum, against the sum of the frames' own counts
+hist = np.bincount(it).tolist()
+lock = {str(g): float(it[: len(it) // g * g].reshape(-1, g).max(axis=1).sum() * g / it[: len(it) // g * g].sum())
+        for g in (2, 4, 8, 16)}
 print(json.dumps({"n": args.n, "m": m, "frames": args.frames, "qber": args.qber, "variant": args.variant,
                   "ms_per_batch": dt * 1e3, "gbit_s": args.frames * args.n / dt / 1e9,
-                  "mean_it": float(it.mean()), "fer": float(1 - r.keys_match.cpu().numpy().mean())}))
+                  "mean_it": float(it.mean()), "iter_hist": hist, "max_it": int(it.max()),
+                  "lockstep_work_ratio": lock, "fer": float(1 - r.keys_match.cpu().numpy().mean())}))

@@ -18,6 +18,7 @@ __global__ __launch_bounds__(1024) void k(float* out, unsigned long long* cyc, i
         y[u] = f2{x[u], x[u] + 0.25f};
         d[u] = (double)x[u];
     }
+    const unsigned long long msk = __builtin_amdgcn_readfirstlane((int)(a > 0.0f)) ? 0x5555555555555555ull : 0ull;
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int i = 0; i < iters; ++i) {
@@ -44,6 +45,9 @@ __global__ __launch_bounds__(1024) void k(float* out, unsigned long long* cyc, i
             if constexpr (OP == 16) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
             if constexpr (OP == 17) asm volatile("v_cmp_gt_f32 vcc, %0, %1" : : "v"(x[u]), "v"(a) : "vcc");
             if constexpr (OP == 18) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            // (the select's mask in an SGPR pair, as the compiler emits it; OP 11
+            // reads VCC, which the loop's own compare may be writing)
+            if constexpr (OP == 19) asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x[u]) : "v"(a), "s"(msk));
         }
     }
     __syncthreads();
@@ -103,6 +107,7 @@ int main() {
         run<16, 8>("v_mul_f32", d, dc, cus, c[0], c[1]);
         run<17, 8>("v_cmp_gt_f32", d, dc, cus, c[0], c[1]);
         run<18, 8>("v_xor_b32", d, dc, cus, c[0], c[1]);
+        run<19, 8>("v_cndmask_b32_sgpr", d, dc, cus, c[0], c[1]);
     }
     return 0;
 }

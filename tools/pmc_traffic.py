@@ -58,6 +58,7 @@ def issue_costs(path=ISSUE_MB, waves=4.0, ilp=8):
 # packed shares per class (census of the paired and iteration-2 check-phase steps
 # and the speculative bit-phase rounds, weighted by their config-2 trip counts)
 PACKED_SHARE = {"FMA_F32": 0.62, "MUL_F32": 0.45, "ADD_F32": 0.63}
+OTHER_KINDS = ("v_mov_b32", "v_xor_b32", "v_bfe_u32", "v_med3_f32", "v_cmp_gt_f32", "v_cndmask_b32_sgpr")
 
 
 def valu_mix(c, cycles):
@@ -78,8 +79,9 @@ def valu_mix(c, cycles):
         "F64": I["v_fma_f64"], "TRANS_F64": 2 * I["v_fma_f64"],
         "INT32": I["v_add_u32"], "INT64": 2 * I["v_add_u32"], "CVT": I["v_add_u32"],
         # the rest (selects, compares, moves, logic, med3 / max, lane reads): the
-        # mean of the measured v_mov, v_xor, v_bfe, v_med3 and v_cmp costs
-        "OTHER": sum(I[k] for k in ("v_mov_b32", "v_xor_b32", "v_bfe_u32", "v_med3_f32", "v_cmp_gt_f32")) / 5,
+        # mean of the measured v_mov, v_xor, v_bfe, v_med3, v_cmp and v_cndmask
+        # (SGPR mask, as compiled) costs
+        "OTHER": sum(I[k] for k in OTHER_KINDS) / len(OTHER_KINDS),
     }
     g = lambda k: c.get("SQ_INSTS_VALU_" + k, 0.0)
     n = {"FMA_F32": g("FMA_F32"), "MUL_F32": g("MUL_F32"), "ADD_F32": g("ADD_F32"), "TRANS_F32": g("TRANS_F32"),
