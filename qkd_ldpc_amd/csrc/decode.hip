@@ -1470,6 +1470,8 @@ static qkd_status ws_free(qkd_workspace* ws) {
     if (ws->low) (void)hipFree(ws->low);
     if (ws->ckpt) (void)hipFree(ws->ckpt);
     if (ws->win) (void)hipFree(ws->win);
+    if (ws->ilv) (void)hipFree(ws->ilv);
+    if (ws->fb_list) (void)hipFree(ws->fb_list);
     if (ws->spec_stat_ev) (void)hipEventSynchronize(ws->spec_stat_ev);
     if (ws->spec_stat_host) (void)hipHostFree(ws->spec_stat_host);
     if (ws->spec_stat_ev) (void)hipEventDestroy(ws->spec_stat_ev);
@@ -1742,6 +1744,48 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 s = check_no_static_lds(sfn);
                 if (s != QKD_OK) return s;
             }
+            // Long codes (the split store keeps under a quarter of the slots
+            // in LDS): the frame-interleaved decoder (decode_ilv.hip), its
+            // hand-offs decoded by this split kernel from a frame list.
+            // QKD_ILV=1 / 0 forces it on / off (tests, A/B).
+            const IlvLds IL(c->m);
+            bool ilv = mode == kModeKeys && spec && !ckpt && !a.bits_out && a.first_table && c->d_ilv_slots &&
+                       IL.bytes <= kLdsBytesMax;
+            if (ilv) {
+                const char* ie = getenv("QKD_ILV");
+                ilv = ie ? atoi(ie) != 0
+                         : (size_t)L.S * 4 < slots && (size_t)a.n_frames * 2 >= (size_t)kIlvCols * c->cu_count;
+            }
+            DecodeFn ifn = nullptr;
+            int igrid = 0;
+            // (per workgroup: the message lines, then the columns' key words)
+            const size_t istride = slots * kIlvCols + (size_t)((c->n + 63) / 64) * kIlvCols * 2;
+            if (ilv) {
+                ifn = pick_ilv(c->ilv_rs, c->max_dc);
+                s = decode_grid(c, ifn, IL.bytes, &igrid);
+                if (s != QKD_OK) return s;
+                igrid = (int)std::min<size_t>((size_t)igrid, ((size_t)a.n_frames + kIlvCols - 1) / kIlvCols);
+                // (QKD_ILV_GRID caps the workgroups: tests take columns through several frames)
+                if (const char* g = getenv("QKD_ILV_GRID")) igrid = std::max(1, std::min(igrid, atoi(g)));
+                const size_t need = (size_t)igrid * istride;
+                if (ws->ilv_elems < need) {
+                    if (ws->ilv) QKD_HIP(hipFree(ws->ilv));
+                    ws->ilv = nullptr;
+                    ws->ilv_elems = 0;
+                    if (hipMalloc(&ws->ilv, need * sizeof(double)) != hipSuccess)
+                        return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate %zu B of interleaved "
+                                                                "message lines", need * sizeof(double));
+                    ws->ilv_elems = need;
+                }
+                if (ws->fb_frames < a.n_frames) {
+                    if (ws->fb_list) QKD_HIP(hipFree(ws->fb_list));
+                    ws->fb_list = nullptr;
+                    ws->fb_frames = 0;
+                    if (hipMalloc(&ws->fb_list, (size_t)a.n_frames * sizeof(uint32_t)) != hipSuccess)
+                        return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate the hand-off list");
+                    ws->fb_frames = a.n_frames;
+                }
+            }
             // [0] frame queue, [1] replays: zeroed by frame_syn_kernel on the
             // keys path (it runs first on this stream: block 0 writes both
             // words), by a memset otherwise -- one branch, so a keys-mode
@@ -1758,7 +1802,27 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 if (a.win) QKD_HIP(hipMemsetAsync(a.win, 0, 2 * (size_t)a.win_count * sizeof(uint32_t), stream));
             }
             QKD_HIP(decoder_event(ws, stream));
-            hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
+            if (ilv) {
+                // [2] the hand-off queue, [3] the hand-off count
+                QKD_HIP(hipMemsetAsync(ws->counter + 2, 0, 8, stream));
+                DecodeArgs ai = a;
+                ai.ilv_store = ws->ilv;
+                ai.ilv_stride = istride;
+                ai.fb_list = ws->fb_list;
+                ai.fb_count = ws->counter + 3;
+                hipLaunchKernelGGL(ifn, dim3(igrid), dim3(kDecodeBlock), IL.bytes, stream, ai);
+                // the hand-offs: speculating again, exact replays in place (no
+                // in-launch policy: its windows count frame indices)
+                DecodeArgs af = a;
+                af.counter = ws->counter + 2;
+                af.frame_list = ws->fb_list;
+                af.frame_count = ws->counter + 3;
+                af.spec_always = 1;
+                if (hipGetLastError() == hipSuccess)
+                    hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, af);
+            } else {
+                hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
+            }
             QKD_HIP(decoder_event_close(ws, stream, hipGetLastError()));
             if (mode == kModeKeys) QKD_HIP(launch_key_match(a, stream));
             return QKD_OK;

@@ -1112,8 +1112,15 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
         const int k = window_of(fr);
         return k < 0 ? 0ull : __hip_atomic_load(win64 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
+    // the next frame of the queue: frame k, or with a frame list (the
+    // interleaved decoder's hand-offs, decode_ilv.hip) its k-th entry
+    auto claim = [&]() -> uint32_t {
+        const uint32_t k = atomicAdd(a.counter, 1u);
+        if (a.frame_list == nullptr) return k;
+        return k < *a.frame_count ? a.frame_list[k] : a.n_frames;
+    };
     if (tid == 0) {
-        ctl[1] = atomicAdd(a.counter, 1u);
+        ctl[1] = claim();
         ctl[6] = spec_policy(ctl[1], window_peek(ctl[1]));
     }
     uint32_t next_f = 0;
@@ -1126,7 +1133,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
         __syncthreads();
         const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl[1]);   // (uniform to the compiler)
         if (f >= a.n_frames) break;
-        if (tid == 0) next_f = atomicAdd(a.counter, 1u);
+        if (tid == 0) next_f = claim();
         // this frame's replay events (thread 0; the policy's window count)
         uint32_t frame_replays = 0;
 

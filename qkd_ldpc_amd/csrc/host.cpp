@@ -47,10 +47,12 @@ static void free_device(qkd_code* c) {
     c->d_bit_code = nullptr;
     if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
     for (void* p : {(void*)c->d_perm, (void*)c->d_inv, (void*)c->d_bit_chk_s, (void*)c->d_bit_deg_s,
-                    (void*)c->d_bit_pat_s, (void*)c->d_chk_rows16})
+                    (void*)c->d_bit_pat_s, (void*)c->d_chk_rows16, (void*)c->d_ilv_slots})
         if (p) (void)hipFree(p);
     c->d_chk_rows16 = nullptr;
     c->chk_rs = 0;
+    c->d_ilv_slots = nullptr;
+    c->ilv_rs = 0;
     c->d_perm = c->d_inv = c->d_bit_chk_s = nullptr;
     c->d_bit_deg_s = nullptr;
     c->d_bit_pat_s = nullptr;
@@ -405,6 +407,16 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
         }
         QKD_HIP(hipMalloc(&c->d_bit_code, code.size() * sizeof(uint64_t)));
         QKD_HIP(hipMemcpy(c->d_bit_code, code.data(), code.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+        // the frame-interleaved decoder's check rows (decode_ilv.hip): each
+        // edge's message line, row * n_pad + internal bit, in the check's order
+        const int32_t rs = max_dc <= 8 ? 8 : 16;
+        std::vector<uint32_t> lines((size_t)m * rs, 0xffffffffu);
+        for (int32_t j = 0; j < m; ++j)
+            for (int32_t k = cptr[j]; k < cptr[j + 1]; ++k)
+                lines[(size_t)j * rs + (k - cptr[j])] = (uint32_t)krow[k] * (uint32_t)c->n_pad + (uint32_t)inv[cidx[k]];
+        QKD_HIP(hipMalloc(&c->d_ilv_slots, lines.size() * sizeof(uint32_t)));
+        QKD_HIP(hipMemcpy(c->d_ilv_slots, lines.data(), lines.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        c->ilv_rs = rs;
     }
     }   // split
     std::vector<uint2> plan2(plan.word.size());

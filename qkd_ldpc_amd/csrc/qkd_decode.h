@@ -159,6 +159,38 @@ struct DecodeArgs {
     double* ckpt;
     uint32_t ckpt_stride;
     uint32_t ckpt_unsat;
+    // the frame-interleaved decoder (decode_ilv.hip): its message lines
+    // (ilv_stride doubles per workgroup) and the frames whose intervals could
+    // not certify, for the split kernel (fb_list, fb_count entries)
+    double* ilv_store;
+    size_t ilv_stride;
+    uint32_t* fb_list;
+    uint32_t* fb_count;
+    // decode_split_kernel: decode only frame_list[0 .. *frame_count) (the
+    // interleaved decoder's hand-offs), or every frame when nullptr
+    const uint32_t* frame_list;
+    const uint32_t* frame_count;
+};
+
+// The frame-interleaved decoder (decode_ilv.hip): kIlvCols frames per
+// workgroup in lockstep, one per lane of each 16-lane group; one message
+// line = one slot of the kIlvCols frames (128 bytes).
+constexpr int kIlvCols = 16;
+constexpr int kIlvCtlWords = 64;
+// LDS: tsyn / xsyn / xunc, one word per check pair (check 2w in bits 0-15,
+// 2w + 1 in bits 16-31, bit = column), the column control words, the
+// first-iteration magnitudes by check degree.
+struct IlvLds {
+    size_t tsyn, xsyn, xunc, ctl, ctab, bytes;
+    __host__ __device__ explicit IlvLds(int m) {
+        const size_t mw2 = (size_t)(m + 1) / 2;
+        tsyn = 0;
+        xsyn = mw2 * 4;
+        xunc = 2 * mw2 * 4;
+        ctl = (3 * mw2 * 4 + 15) & ~(size_t)15;
+        ctab = ctl + (size_t)kIlvCtlWords * 4;
+        bytes = ctab + (size_t)(kFirstTableDeg + 1) * 8;
+    }
 };
 
 // Phase-clock accumulation (diagnostic; a wave-uniform test when off). Each
@@ -590,6 +622,8 @@ DecodeFn pick_split_decode(int mode, int rule, bool clamp, int max_dc, int* dc);
 // checkpointed variant (keys path: exact iterations first, interval ones from
 // a checkpoint once few checks are unsatisfied).
 DecodeFn pick_split_spec(int mode, int max_dc, bool ckpt, int* dc);
+// the frame-interleaved decoder (decode_ilv.hip) for check-row stride rs (8 or 16)
+DecodeFn pick_ilv(int rs, int max_dc);
 // decode_split.hip, kModeKeys: the kernels around the split decoder.
 // Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.
 hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream);

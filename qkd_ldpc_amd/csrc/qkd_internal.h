@@ -113,6 +113,12 @@ struct DeviceCode {
     // past the row; chk_rs 8 or 16)
     const uint16_t* chk_rows16;
     int32_t chk_rs;
+    // the frame-interleaved decoder (decode_ilv.hip; split view, bit_code
+    // present, check degree <= 16): ilv_slots[j * ilv_rs + k] = the message
+    // line (row * n_pad + internal bit) of the k-th edge of check j, ~0 past
+    // its degree (ilv_rs 8 or 16); nullptr otherwise
+    const uint32_t* ilv_slots;
+    int32_t ilv_rs;
 };
 
 }  // namespace qkd
@@ -166,6 +172,13 @@ struct qkd_workspace {
     // the speculative kernel's in-launch policy windows (DecodeArgs::win)
     uint32_t* win = nullptr;
     size_t win_words = 0;
+    // the frame-interleaved decoder (decode_ilv.hip): message lines of every
+    // resident workgroup (16 frames per 128-byte line), and the frames it
+    // hands to the split kernel's exact replays
+    double* ilv = nullptr;
+    size_t ilv_elems = 0;
+    uint32_t* fb_list = nullptr;
+    size_t fb_frames = 0;
     // qkd_debug_decoder_timing: while on, HIP events bracket every decoder
     // launch on its stream (pairs recorded, read back on collection)
     bool time_decoder = false;
@@ -207,6 +220,8 @@ struct qkd_code {
     // frame_syn_sliced_kernel's compact check rows (host.cpp)
     uint16_t* d_chk_rows16 = nullptr;
     int32_t chk_rs = 0;
+    uint32_t* d_ilv_slots = nullptr;
+    int32_t ilv_rs = 0;
     int32_t* d_bit_chk_s = nullptr;
     uint8_t* d_bit_deg_s = nullptr;
     uint16_t* d_bit_pat_s = nullptr;
@@ -231,14 +246,14 @@ struct qkd_code {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
                                n_pat, d_bit_pat, d_pat_deg, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, 0};
+                               nullptr, 0, nullptr, 0};
     }
     // the split kernels' view (internal bit order, DeviceCode::perm)
     qkd::DeviceCode view_split() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk_s, nullptr, d_bit_deg_s,
                                n_pat, d_bit_pat_s, d_pat_deg, d_bit_code, d_plan_slot, d_perm, d_inv,
-                               d_chk_rows16, chk_rs};
+                               d_chk_rows16, chk_rs, d_ilv_slots, ilv_rs};
     }
 };
 

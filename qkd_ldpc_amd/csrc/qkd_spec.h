@@ -283,6 +283,50 @@ __device__ __forceinline__ void psi_of_exact2(double b0, double b1, f2& r0, f2& 
     r1 = ok1 ? (n1 ? -ph1.yx : ph1) : f2{nan, nan};
 }
 
+// phi_bounds of two intervals [a.x, a.y] and [b.x, b.y] in one packed
+// evaluation (the operations of psi_of_exact2's core: each half bit for bit
+// phi_bounds). The frame-interleaved check phase (decode_ilv.hip) pairs its
+// edges with it.
+__device__ __forceinline__ void phi_bounds2(f2 a, f2 b, f2& ra, f2& rb) {
+    const f2 x = f2{__builtin_amdgcn_fmed3f(a.x, 0.0f, kPhiHuge), __builtin_amdgcn_fmed3f(b.x, 0.0f, kPhiHuge)};
+    const float L = 1.44269502162933349609375f;
+    const float L_lo = 1.925963033500011079e-08f;
+    const f2 p = x * f2(L);
+    const f2 rl = __builtin_elementwise_fma(__builtin_elementwise_fma(x, f2(L), -p), f2(kLn2), x * f2(L_lo * kLn2));
+    const f2 e2 = f2{__builtin_amdgcn_exp2f(-p.x), __builtin_amdgcn_exp2f(-p.y)};
+    const f2 u = __builtin_elementwise_fma(e2, -rl, e2);
+    const PhiVal2 e = phi_core_pair<true>(x, u, f2{__builtin_amdgcn_logf(x.x), __builtin_amdgcn_logf(x.y)});
+    const f2 hi = __builtin_elementwise_fma(e.v, f2(kPhiRel), e.v) + f2(1.0e-37f);
+    const f2 t = __builtin_elementwise_fma(-e.slope * f2((1.0f + 2.0f * kPhiRel) * kInvLn2), f2{a.y, b.y} - x,
+                                           e.v * f2(1.0f - kPhiRel));
+    ra = f2{t.x > 0.0f ? t.x : 0.0f, hi.x};
+    rb = f2{t.y > 0.0f ? t.y : 0.0f, hi.y};
+}
+
+// phi_bounds_out of two psi-unit sums [s.x, s.y] and [r.x, r.y] in one packed
+// evaluation: phi_core<false, true>'s operations elementwise, each half bit
+// for bit phi_bounds_out.
+__device__ __forceinline__ void phi_bounds_out2(f2 s, f2 r, f2& os, f2& orr) {
+    const bool z0 = !(s.x > 0.0f), z1 = !(r.x > 0.0f);
+    const f2 at = f2{__builtin_fminf(z0 ? s.y : s.x, kPsiHuge), __builtin_fminf(z1 ? r.y : r.x, kPsiHuge)};
+    const f2 x = at * f2(kLn2);
+    const f2 u = f2{__builtin_amdgcn_exp2f(-at.x), __builtin_amdgcn_exp2f(-at.y)};
+    const f2 lg = f2{__builtin_amdgcn_logf(at.x), __builtin_amdgcn_logf(at.y)};
+    const f2 g = series_g(x * x);
+    const f2 t = __builtin_elementwise_fma(f2(-kLn2), lg, f2(kPhiK));
+    const f2 vlo = __builtin_elementwise_fma(g, f2(1.0f), t);
+    const f2 h = series_h(u * u);
+    const f2 vhi = (u * f2(2.0f)) * h;
+    const f2 v = f2{x.x < 1.0f ? vlo.x : vhi.x, x.y < 1.0f ? vlo.y : vhi.y};
+    const f2 sh = f2(2.32f) * u;
+    const f2 slope = f2{x.x < 1.0f ? __builtin_amdgcn_rcpf(x.x) : sh.x, x.y < 1.0f ? __builtin_amdgcn_rcpf(x.y) : sh.y};
+    const f2 vmax = __builtin_elementwise_fma(v, f2(kPhiRel), v) + f2(1.0e-37f);
+    const f2 tn = __builtin_elementwise_fma(-slope * f2((1.0f + 2.0f * kPhiRel) * kLn2), f2{s.y, r.y} - at,
+                                            v * f2(1.0f - kPhiRel));
+    os = f2{tn.x > 0.0f ? tn.x : 0.0f, z0 ? __builtin_inff() : vmax.x};
+    orr = f2{tn.y > 0.0f ? tn.y : 0.0f, z1 ? __builtin_inff() : vmax.y};
+}
+
 // An interval travels through the double-width message slots as its bits.
 __device__ __forceinline__ double pack_iv(f2 v) { return __builtin_bit_cast(double, v); }
 __device__ __forceinline__ f2 unpack_iv(double v) { return __builtin_bit_cast(f2, v); }

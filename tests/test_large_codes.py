@@ -158,3 +158,45 @@ def test_frame_syn_sliced_equals_plain(monkeypatch, dv, dc, n):
     x, y = out["1"], out["0"]
     assert torch.equal(x.iterations, y.iterations) and torch.equal(x.bits, y.bits)
     assert torch.equal(x.keys_match, y.keys_match) and torch.equal(x.syndromes_match, y.syndromes_match)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,grid", [(0.03, 1), (0.05, 2), (0.08, 3)])
+def test_interleaved_trials_equal_oracle(Q, big_codes, oracle_mod, monkeypatch, q, grid):
+    """The frame-interleaved decoder (decode_ilv.hip, forced with QKD_ILV=1)
+    against the oracle: 40 frames through 1-3 workgroups, so columns take
+    several frames each (the queue refill); at q = 0.08 frames hand off to the
+    split kernel's exact replays."""
+    monkeypatch.setenv("QKD_ILV", "1")
+    monkeypatch.setenv("QKD_ILV_GRID", str(grid))
+    H, oc = big_codes
+    seeds = oracle_mod.seeds(123, 40)
+    r = Q.run_trials(H, torch.from_numpy(seeds.view(np.int64)).cuda(), q, 0, 40)
+    torch.cuda.synchronize()
+    want = oc.trials(q, seeds, 0, 40, 100.0, True)
+    assert (r.iterations.cpu().numpy() == want["iters"]).all()
+    assert (r.syndromes_match.cpu().numpy().astype(bool) == want["sp_ok"]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == want["key_ok"]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,cap", [(0.02, None), (0.03, None), (0.03, "2"), (0.05, None)])
+def test_interleaved_equals_split_at_scale(Q, big_codes, monkeypatch, q, cap):
+    """4096 frames: the interleaved decoder (its default for this code at this
+    batch size) and the split kernel (QKD_ILV=0) give the same iterations,
+    syndrome and key flags. QKD_SPEC_CAP=2 hands every frame still iterating
+    after two interval rounds to the split kernel (its frame-list path)."""
+    H, _ = big_codes
+    if cap:
+        monkeypatch.setenv("QKD_SPEC_CAP", cap)
+    seeds = torch.from_numpy(Q.make_seeds(2024, 4096).view(np.int64)).cuda()
+    a, b, qq = Q.keygen(H, seeds, q)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("QKD_ILV", mode)
+        r = Q.qkd_ldpc(H, a, b, float(qq[0]), 50)
+        torch.cuda.synchronize()
+        out[mode] = r
+    x, y = out["1"], out["0"]
+    assert torch.equal(x.iterations, y.iterations)
+    assert torch.equal(x.syndromes_match, y.syndromes_match) and torch.equal(x.keys_match, y.keys_match)
