@@ -1762,8 +1762,11 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             const size_t istride = slots * kIlvCols + (size_t)((c->n + 63) / 64) * kIlvCols * 2;
             if (ilv) {
                 ifn = pick_ilv(c->ilv_rs, c->max_dc);
-                s = decode_grid(c, ifn, IL.bytes, &igrid);
-                if (s != QKD_OK) return s;
+                QKD_HIP(hipFuncSetAttribute((const void*)ifn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)IL.bytes));
+                int per_cu = 0;
+                QKD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ifn, kIlvBlock, IL.bytes));
+                if (per_cu < 1) return set_error(QKD_ERR_UNSUPPORTED, "interleaved decoder cannot be resident");
+                igrid = per_cu * c->cu_count;
                 igrid = (int)std::min<size_t>((size_t)igrid, ((size_t)a.n_frames + kIlvCols - 1) / kIlvCols);
                 // (QKD_ILV_GRID caps the workgroups: tests take columns through several frames)
                 if (const char* g = getenv("QKD_ILV_GRID")) igrid = std::max(1, std::min(igrid, atoi(g)));
@@ -1810,7 +1813,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 ai.ilv_stride = istride;
                 ai.fb_list = ws->fb_list;
                 ai.fb_count = ws->counter + 3;
-                hipLaunchKernelGGL(ifn, dim3(igrid), dim3(kDecodeBlock), IL.bytes, stream, ai);
+                hipLaunchKernelGGL(ifn, dim3(igrid), dim3(kIlvBlock), IL.bytes, stream, ai);
                 // the hand-offs: the split kernel's exact iterations (their
                 // intervals could not certify; speculating again measured 1.7x
                 // slower), through the frame list

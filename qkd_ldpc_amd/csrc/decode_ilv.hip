@@ -39,9 +39,15 @@
 
 namespace qkd {
 
+// checks of lines in flight per group while one computes (2 needs the
+// registers of a 512-thread workgroup)
+#ifndef QKD_ILV_AHEAD
+#define QKD_ILV_AHEAD (QKD_ILV_BLOCK <= 512 ? 2 : 1)
+#endif
+
 namespace {
 
-constexpr int kIlvGroups = kDecodeBlock / kIlvCols;     // 16-lane groups per workgroup
+constexpr int kIlvGroups = kIlvBlock / kIlvCols;     // 16-lane groups per workgroup
 
 // ctl words (IlvLds::ctl)
 constexpr int kCtlFrame = 0;      // [16] frame of each column (n_frames: none)
@@ -52,6 +58,7 @@ constexpr int kCtlKeyMis = 34;    // this round: columns whose decision differs 
 constexpr int kCtlMis = 35;       // this round: columns with a check certainly unsatisfied
 constexpr int kCtlUnc = 36;       // this round: columns with a check whose parity is uncertain
 constexpr int kCtlRefill = 37;    // columns given a new frame (their target syndromes to load)
+constexpr int kCtlIvl = 38;       // columns in an interval iteration (check phase runs)
 
 __device__ __forceinline__ qkds::f2 neg_if(bool neg, qkds::f2 v) {
     return qkds::f2{neg ? -v.y : v.x, neg ? -v.x : v.y};
@@ -67,7 +74,7 @@ __device__ __forceinline__ uint32_t fold_groups(uint64_t b) {
 // RS: the row stride of DeviceCode::ilv_slots; DM: the largest check degree
 // rounded up to even (the register arrays' size)
 template <int RS, int DM>
-__global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) {
+__global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     static_assert(DM <= RS && DM % 2 == 0, "degree bucket");
     using qkds::f2;
     extern __shared__ __align__(16) unsigned char smem[];
@@ -83,17 +90,32 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
     uint32_t* xunc = reinterpret_cast<uint32_t*>(smem + L.xunc);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
+    uint32_t* ilv_ring = reinterpret_cast<uint32_t*>(smem + L.ring);
     const uint32_t m_words = (uint32_t)decode_m_words(c.m);
     const uint32_t n_pad = (uint32_t)c.n_pad;
     double* const lines = a.ilv_store + (size_t)blockIdx.x * a.ilv_stride;
     // after the lines: the columns' key words, interleaved ([word][column]
     // {bob, alice}), copied at each refill
     uint4* const keyi = reinterpret_cast<uint4*>(lines + (size_t)c.max_dv * n_pad * kIlvCols);
+    // The lines through a buffer descriptor: a line index of ~0 (an edge past
+    // the check's degree, a row past the bit's) gives an offset past the
+    // region, which loads 0 and drops the store -- no branch around any
+    // access (a branch there made the compiler wait for every load in flight
+    // at the top of each pipelined loop)
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(
+        lines, (short)0, (int)((size_t)c.max_dv * n_pad * kIlvCols * sizeof(double)), 0x00020000);
+    using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(lrs, 0, 0, 0));
+    auto ld_line = [&](uint32_t x) -> double {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lrs, (int)(x * 128u + col * 8u), 0, 0));
+    };
+    auto st_line = [&](uint32_t x, double v) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), lrs, (int)(x * 128u + col * 8u), 0, 0);
+    };
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
     const double llr_p = a.log_p;
 
-    for (int d = tid; d <= kFirstTableDeg; d += kDecodeBlock) ctab[d] = a.first_c2b[d];
-    for (uint32_t w = (uint32_t)tid; w < mw2; w += kDecodeBlock) {
+    for (int d = tid; d <= kFirstTableDeg; d += kIlvBlock) ctab[d] = a.first_c2b[d];
+    for (uint32_t w = (uint32_t)tid; w < mw2; w += kIlvBlock) {
         tsyn[w] = 0;
         xsyn[w] = 0;
         xunc[w] = 0;
@@ -126,7 +148,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
     auto refill = [&]() {
         const uint32_t rf = ctl[kCtlRefill];
         if (rf == 0) return;
-        for (uint32_t w = (uint32_t)tid; w < mw2; w += kDecodeBlock) {
+        for (uint32_t w = (uint32_t)tid; w < mw2; w += kIlvBlock) {
             uint32_t v = tsyn[w];
             for (uint32_t r = rf; r != 0; r &= r - 1u) {
                 const uint32_t cc = (uint32_t)__builtin_ctz(r);
@@ -140,7 +162,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
         for (uint32_t r = rf; r != 0; r &= r - 1u) {
             const uint32_t cc = (uint32_t)__builtin_ctz(r);
             const uint32_t f = ctl[kCtlFrame + cc];
-            for (uint32_t w = (uint32_t)tid; w < a.words; w += kDecodeBlock) {
+            for (uint32_t w = (uint32_t)tid; w < a.words; w += kIlvBlock) {
                 const uint64_t b = a.bob_w[(size_t)f * a.words + w], al = a.alice_w[(size_t)f * a.words + w];
                 keyi[(size_t)w * kIlvCols + cc] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)al,
                                                              (uint32_t)(al >> 32));
@@ -160,57 +182,84 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
         const bool act = (active >> col) & 1u;
 
         // ---- check phase (columns past their folded first iteration).
-        // Software-pipelined over the group's checks j, j + G, ...: the lines of
-        // the next check are loaded while this one computes, its line indices
-        // a check earlier still.
+        // Software-pipelined over the group's checks t = 0, 1, ... (check j =
+        // grp + t G): the lines of check t + 1 are in flight while check t
+        // computes; each check's line indices go through a four-stage LDS
+        // ring of the group (one copy per group instead of a register per
+        // lane), loaded from global memory three checks ahead.
         bool bad = false;
-        if (act && it != 0) {
-            auto load_idx = [&](int jj, uint32_t (&x)[DM], int& deg) {
-                deg = 0;
-#pragma unroll
-                for (int k = 0; k < DM; ++k) x[k] = 0;
-                if (jj < c.m) {
-                    deg = c.chk_deg[jj];
-                    const uint2* sl = reinterpret_cast<const uint2*>(c.ilv_slots + (size_t)jj * RS);
-#pragma unroll
-                    for (int q = 0; q < DM / 2; ++q) {
-                        const uint2 u = sl[q];
-                        x[2 * q] = u.x;
-                        x[2 * q + 1] = u.y;
-                    }
-                }
+        // (every lane of a group keeps the ring, whatever its column's state:
+        // the lanes that write an index are fixed columns; lanes of columns
+        // not in an interval iteration load and store nothing, ~0)
+        const bool part = act && it != 0;
+        if (__builtin_amdgcn_readfirstlane((int)ctl[kCtlIvl]) != 0) {
+            uint32_t* ring = ilv_ring + grp * (4 * kRingStage);
+            // lane col < DM: line index col of check jj (~0 past its degree,
+            // DeviceCode::ilv_slots, and past the last check)
+            // (a clamped, unconditional load and a select: a branch around a
+            // load or store makes the compiler drain every load in flight)
+            // (the raw load; the validity select waits until the commit a
+            // step later, so nothing consumes the value right after its load)
+            auto idx_issue = [&](int jj) -> uint32_t {
+                const int jq = jj < c.m ? jj : c.m - 1;
+                return c.ilv_slots[(size_t)jq * RS + (col < (uint32_t)DM ? col : 0u)];
             };
-            auto load_lines = [&](const uint32_t (&x)[DM], int deg, double (&v)[DM]) {
-#pragma unroll
-                for (int k = 0; k < DM; ++k) v[k] = k < deg ? lines[(size_t)x[k] * kIlvCols + col] : 0.0;
+            auto idx_commit = [&](int t, uint32_t r) {
+                const bool ok = grp + t * kIlvGroups < c.m;
+                if (col < (uint32_t)DM) ring[(t & 3) * kRingStage + col] = ok ? r : ~0u;
             };
-            uint32_t xa[DM], xb[DM];
-            int dega, degb;
-            double va[DM];
-            int j = grp;
-            load_idx(j, xa, dega);
-            load_lines(xa, dega, va);
-            load_idx(j + kIlvGroups, xb, degb);
-            while (j < c.m) {
-                double vb[DM];
-                load_lines(xb, degb, vb);
-                uint32_t xc[DM];
-                int degc;
-                load_idx(j + 2 * kIlvGroups, xc, degc);
+            auto lines_issue = [&](int t, double (&v)[DM]) {
+                const uint32_t* st = ring + (t & 3) * kRingStage;
+#pragma unroll
+                for (int k = 0; k < DM; ++k) v[k] = ld_line(part ? st[k] : ~0u);
+            };
+            const int nt = (c.m - grp + kIlvGroups - 1) / kIlvGroups;     // this group's checks
+            // (memory operations complete in issue order for the waits: each
+            // iteration issues the index load it commits next, then the lines
+            // two checks ahead, then commits the indices loaded one iteration
+            // earlier -- whose wait covers check t's lines only)
+            idx_commit(0, idx_issue(grp));
+            idx_commit(1, idx_issue(grp + kIlvGroups));
+            idx_commit(2, idx_issue(grp + 2 * kIlvGroups));
+            uint32_t rnext = idx_issue(grp + 3 * kIlvGroups);
+            double va[DM], vb[DM];
+            lines_issue(0, va);
+#if QKD_ILV_AHEAD == 2
+            double vc[DM];
+            lines_issue(1, vb);
+#endif
+            // one check: t's lines in `cur`, t + 1's issued into `ld`. The loop
+            // runs it unrolled twice over two register sets, so no line value
+            // is copied between iterations (a copy waits for the load it
+            // copies, which would drain the pipeline every check; a third set
+            // for two checks ahead spills at this occupancy)
+            // (rc: the indices of check t + 3, loaded a step earlier; rl: those
+            // of check t + 4, loaded now -- two registers alternating, no copy)
+            auto step = [&](int t, const double (&cur)[DM], double (&ld)[DM], const uint32_t& rc,
+                            uint32_t& rl) -> bool {
+                if (t >= nt) return false;
+                const int j = grp + t * kIlvGroups;
+                rl = idx_issue(j + 4 * kIlvGroups);
+                lines_issue(t + QKD_ILV_AHEAD, ld);
+                idx_commit(t + 3, rc);
+                const uint32_t* st = ring + (t & 3) * kRingStage;
+                uint32_t live = 0;          // bit k: edge k exists
+#pragma unroll
+                for (int k = 0; k < DM; ++k) live |= (st[k] != ~0u ? 1u : 0u) << k;
                 // |b2c| bounds (psi units) and signs, two edges per packed
                 // evaluation (spec_check_phase_paired's input bounds)
                 f2 ph[DM];
                 uint32_t negs = 0;
 #pragma unroll
                 for (int k = 0; k < DM; k += 2) {
-                    const f2 b0 = qkds::unpack_iv(va[k]), b1 = qkds::unpack_iv(va[k + 1]);
+                    const f2 b0 = qkds::unpack_iv(cur[k]), b1 = qkds::unpack_iv(cur[k + 1]);
                     const bool n0 = b0.y < 0.0f, n1 = b1.y < 0.0f;
                     const f2 a0 = neg_if(n0, b0), a1 = neg_if(n1, b1);
                     const bool ok0 = a0.x > 1.0e-30f, ok1 = a1.x > 1.0e-30f;
-                    f2 r0 = f2{0.0f, 0.0f}, r1 = f2{0.0f, 0.0f};
-                    if (k < dega) qkds::phi_bounds2(a0, a1, r0, r1);
-                    const bool in0 = k < dega, in1 = k + 1 < dega;
-                    bad |= (in0 && !ok0) || (in1 && !ok1);
+                    f2 r0, r1;
+                    const bool in0 = (live >> k) & 1u, in1 = (live >> (k + 1)) & 1u;
+                    qkds::phi_bounds2(a0, a1, r0, r1);
+                    bad |= part && ((in0 && !ok0) || (in1 && !ok1));
                     negs |= (in0 && n0 ? 1u : 0u) << k;
                     negs |= (in1 && n1 ? 1u : 0u) << (k + 1);
                     ph[k] = (in0 && ok0) ? r0 : f2{0.0f, 0.0f};
@@ -218,51 +267,62 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
                 }
                 const uint32_t sbit = (tsyn[j >> 1] >> ((((uint32_t)j & 1u) << 4) + col)) & 1u;
                 const uint32_t par = (uint32_t)__popc(negs) & 1u;
-                // extrinsic sums over the other edges: prefix + suffix (every
-                // term >= 0, zeros past the degree), widened by the binary32
-                // roundings and the reference's binary64 ones (split kernel's)
-                f2 ext[DM];
-                ext[0] = f2{0.0f, 0.0f};
+                // extrinsic sums over the other edges: prefix sums, then a
+                // backward suffix (every term >= 0, zeros past the degree),
+                // widened by the binary32 roundings and the reference's
+                // binary64 ones (the split kernel's); the c2b bounds two edges
+                // per packed evaluation, threshold_matrix (:246-249) on the
+                // magnitude, then the sign
+                f2 pre[DM];
+                pre[0] = f2{0.0f, 0.0f};
 #pragma unroll
-                for (int k = 1; k < DM; ++k) ext[k] = ext[k - 1] + ph[k - 1];
+                for (int k = 1; k < DM; ++k) pre[k] = pre[k - 1] + ph[k - 1];
                 f2 suf = f2{0.0f, 0.0f};
-#pragma unroll
-                for (int k = DM - 1; k >= 0; --k) {
-                    const f2 sum = ext[k] + suf;
+                auto ext_of = [&](int k) -> f2 {
+                    const f2 sum = pre[k] + suf;
                     suf = suf + ph[k];
                     const float mg = __builtin_fmaf(sum.y, (float)(DM + 2) * qkds::kSumRel, qkds::kRefSumAbs);
                     f2 e = sum + f2{-mg, mg};
                     e.x = e.x > 0.0f ? e.x : 0.0f;
-                    bad |= k < dega && !(e.y < qkds::kPsiSumMax);
-                    ext[k] = e;
-                }
-                // the c2b bounds, two edges per packed evaluation; threshold_matrix
-                // (:246-249) on the magnitude, then the sign
+                    bad |= part && ((live >> k) & 1u) && !(e.y < qkds::kPsiSumMax);
+                    return e;
+                };
 #pragma unroll
-                for (int k = 0; k < DM; k += 2) {
-                    if (k < dega) {
+                for (int k = DM - 1; k >= 1; k -= 2) {
+                    const f2 e1 = ext_of(k);
+                    const f2 e0 = ext_of(k - 1);
+                    {
                         f2 m0, m1;
-                        qkds::phi_bounds_out2(ext[k], ext[k + 1], m0, m1);
+                        qkds::phi_bounds_out2(e0, e1, m0, m1);
                         m0.x = __builtin_amdgcn_fmed3f(m0.x, 0.0f, a.thr_dn);
                         m0.y = __builtin_amdgcn_fmed3f(m0.y, 0.0f, a.thr_up);
                         m1.x = __builtin_amdgcn_fmed3f(m1.x, 0.0f, a.thr_dn);
                         m1.y = __builtin_amdgcn_fmed3f(m1.y, 0.0f, a.thr_up);
-                        const uint32_t s0 = sbit ^ par ^ ((negs >> k) & 1u);
-                        const uint32_t s1 = sbit ^ par ^ ((negs >> (k + 1)) & 1u);
-                        lines[(size_t)xa[k] * kIlvCols + col] = qkds::pack_iv(neg_if(s0 != 0u, m0));
-                        if (k + 1 < dega) lines[(size_t)xa[k + 1] * kIlvCols + col] = qkds::pack_iv(neg_if(s1 != 0u, m1));
+                        const uint32_t s0 = sbit ^ par ^ ((negs >> (k - 1)) & 1u);
+                        const uint32_t s1 = sbit ^ par ^ ((negs >> k) & 1u);
+                        // (dropped past the degree: the ring holds ~0 there)
+                        st_line(part ? st[k - 1] : ~0u, qkds::pack_iv(neg_if(s0 != 0u, m0)));
+                        st_line(part ? st[k] : ~0u, qkds::pack_iv(neg_if(s1 != 0u, m1)));
                     }
                 }
-#pragma unroll
-                for (int k = 0; k < DM; ++k) {
-                    xa[k] = xb[k];
-                    xb[k] = xc[k];
-                    va[k] = vb[k];
-                }
-                dega = degb;
-                degb = degc;
-                j += kIlvGroups;
+                return true;
+            };
+            uint32_t rb = 0;
+#if QKD_ILV_AHEAD == 2
+            // (three line sets and three index registers rotating: step t
+            // computes set t % 3 and loads check t + 2 into set (t + 2) % 3)
+            uint32_t rc2 = 0;
+            for (int t = 0;; t += 3) {
+                if (!step(t, va, vc, rnext, rb)) break;
+                if (!step(t + 1, vb, va, rb, rc2)) break;
+                if (!step(t + 2, vc, vb, rc2, rnext)) break;
             }
+#else
+            for (int t = 0;; t += 2) {
+                if (!step(t, va, vb, rnext, rb)) break;
+                if (!step(t + 1, vb, va, rb, rnext)) break;
+            }
+#endif
         }
         {
             const uint32_t bm = fold_groups(__ballot(bad));
@@ -270,20 +330,56 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
         }
         __syncthreads();
 
-        // ---- bit phase
+        // ---- bit phase, software-pipelined over the group's bits i, i + G,
+        // ...: the next bit's code word, key words and lines are loaded
+        // before this bit's arithmetic and stores
         const bool keep = it + 1 < a.max_it;
+        const bool ivl = act && it != 0;
         uint32_t kmis = 0;
-        for (int i = grp; i < c.n; i += kIlvGroups) {
-            const uint64_t bc = c.bit_code[i];
+        struct BitIn {
+            uint64_t bc;
+            uint4 kw;
+            double v[kDvUnroll];
+            uint32_t qw[kDvUnroll];     // folded first iteration: the checks' first-product sign words
+        };
+        // (unconditional loads: a bit index past N reads bit N - 1's words,
+        // unused; a row past the bit's degree or an inactive column reads
+        // through the descriptor's out-of-range offset, 0)
+        // bit ii's code word (two bits ahead), then its key words, lines and
+        // fold words (one bit ahead, from the code word loaded a step
+        // earlier: nothing waits on a load issued in the same step)
+        auto bit_load_bc = [&](int ii, BitIn& b) { b.bc = c.bit_code[ii < c.n ? ii : c.n - 1]; };
+        auto bit_load = [&](int ii, BitIn& b) {
+            const int iq = ii < c.n ? ii : c.n - 1;
+            b.kw = keyi[(size_t)(iq >> 6) * kIlvCols + col];
+            // (every row's line, not just the bit's degree's: rows past the
+            // degree are read and never used)
+#pragma unroll
+            for (int k = 0; k < kDvUnroll; ++k) {
+                b.v[k] = ld_line((ivl && k < c.max_dv) ? (uint32_t)k * n_pad + (uint32_t)iq : ~0u);
+                // (word 0 of the array when not folding: one cached line for all)
+                const uint32_t j = (uint32_t)(b.bc >> (16 * k)) & 0xffffu;
+                b.qw[k] = a.synw[(act && it == 0) ? (size_t)f * 2 * m_words + m_words + (j >> 5) : 0];
+            }
+        };
+        // one bit: `cur` holds bit i's inputs, the next bit's go into `ld`;
+        // unrolled twice over two input sets (no copies, as the check phase)
+        auto bstep = [&](int i, BitIn& cur, BitIn& ld) -> bool {
+            if (i >= c.n) return false;
+            bit_load(i + kIlvGroups, ld);
+            const uint64_t bc = cur.bc;
+            bit_load_bc(i + 2 * kIlvGroups, cur);
             const int deg = (int)(bc >> 48) & 3;
             int32_t jc[kDvUnroll];
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k) jc[k] = (int32_t)(bc >> (16 * k)) & 0xffff;
+            // (every lane computes, inactive columns' results masked: no
+            // branch around the stores)
             bool z = false, unc = false, dif = false;
-            if (act) {
+            {
                 // (this column's Bob and Alice words of bit i, from the
                 // workgroup's interleaved copy: one 256-byte run per group)
-                const uint4 kw = keyi[(size_t)(i >> 6) * kIlvCols + col];
+                const uint4 kw = cur.kw;
                 const uint64_t bw = ((uint64_t)kw.y << 32) | kw.x, aw = ((uint64_t)kw.w << 32) | kw.z;
                 const uint32_t bob = (uint32_t)(bw >> (i & 63)) & 1u;
                 f2 bo[kDvUnroll];
@@ -296,8 +392,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k) {
                         const int j = jc[k];
-                        const uint32_t qw = a.synw[(size_t)f * 2 * m_words + m_words + ((uint32_t)j >> 5)];
-                        const uint32_t sp = (qw >> (j & 31)) & 1u;
+                        const uint32_t sp = (cur.qw[k] >> (j & 31)) & 1u;
                         const double cm = ctab[((uint32_t)(bc >> (50 + 4 * k)) & 15u) + 1u];
                         cv[k] = k < deg ? ((sp ^ sgi) ? -cm : cm) : 0.0;
                     }
@@ -316,8 +411,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
                     float mag = amax(L);
 #pragma unroll
                     for (int k = 0; k < kDvUnroll; ++k) {
-                        cs[k] = k < deg ? qkds::unpack_iv(lines[((size_t)k * n_pad + (uint32_t)i) * kIlvCols + col])
-                                        : f2{0.0f, 0.0f};
+                        cs[k] = k < deg ? qkds::unpack_iv(cur.v[k]) : f2{0.0f, 0.0f};
                         T = T + cs[k];
                         mag = mag + amax(cs[k]);
                     }
@@ -337,12 +431,12 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
                     }
                 }
                 const uint32_t al = (uint32_t)(aw >> (i & 63)) & 1u;
-                dif = (uint32_t)z != al;
-                if (keep) {
+                z = act && z;
+                unc = act && unc;
+                dif = act && (uint32_t)z != al;
 #pragma unroll
-                    for (int k = 0; k < kDvUnroll; ++k)
-                        if (k < deg) lines[((size_t)k * n_pad + (uint32_t)i) * kIlvCols + col] = qkds::pack_iv(bo[k]);
-                }
+                for (int k = 0; k < kDvUnroll; ++k)
+                    st_line((act && keep && k < deg) ? (uint32_t)k * n_pad + (uint32_t)i : ~0u, qkds::pack_iv(bo[k]));
             }
             // the group's 16 columns' decisions: one syndrome atomic per check
             const uint32_t sh = (uint32_t)lane & 48u;
@@ -359,6 +453,15 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
                     }
                 }
             }
+            return true;
+        };
+        BitIn ba, bb;
+        bit_load_bc(grp, ba);
+        bit_load(grp, ba);
+        bit_load_bc(grp + kIlvGroups, bb);
+        for (int i = grp;; i += 2 * kIlvGroups) {
+            if (!bstep(i, ba, bb)) break;
+            if (!bstep(i + kIlvGroups, bb, ba)) break;
         }
         if (lane == 0 && kmis) atomicOr(ctl + kCtlKeyMis, kmis);
         __syncthreads();
@@ -366,7 +469,7 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
         // ---- syndrome test (:285): per column, a check certainly unsatisfied
         // and a check whose parity is uncertain; xsyn / xunc cleared
         uint32_t mis = 0, un = 0;
-        for (uint32_t w = (uint32_t)tid; w < mw2; w += kDecodeBlock) {
+        for (uint32_t w = (uint32_t)tid; w < mw2; w += kIlvBlock) {
             const uint32_t u = xunc[w];
             const uint32_t d = (xsyn[w] ^ tsyn[w]) & ~u;
             mis |= d | (d >> 16);
@@ -423,6 +526,10 @@ __global__ __launch_bounds__(kDecodeBlock) void decode_ilv_kernel(DecodeArgs a) 
                 ctl[kCtlRefill] = 0;
             }
             if (need) assign(need);
+            // the columns whose next round is an interval one
+            const bool iv = lane < kIlvCols && ((ctl[kCtlActive] >> lane) & 1u) && ctl[kCtlIt + lane] != 0;
+            const uint32_t ivm = (uint32_t)__ballot(iv) & 0xffffu;
+            if (lane == 0) ctl[kCtlIvl] = ivm;
         }
         __syncthreads();
         refill();

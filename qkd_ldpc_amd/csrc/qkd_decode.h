@@ -177,11 +177,19 @@ struct DecodeArgs {
 // line = one slot of the kIlvCols frames (128 bytes).
 constexpr int kIlvCols = 16;
 constexpr int kIlvCtlWords = 64;
+// its workgroup size (QKD_ILV_BLOCK; one workgroup per CU either way: its LDS)
+#ifndef QKD_ILV_BLOCK
+#define QKD_ILV_BLOCK 1024
+#endif
+constexpr int kIlvBlock = QKD_ILV_BLOCK;
+// the check phase's index ring: per 16-lane group four stages of kRingStage
+// words (a check's line indices, ~0 past its degree)
+constexpr int kRingStage = 16;
 // LDS: tsyn / xsyn / xunc, one word per check pair (check 2w in bits 0-15,
 // 2w + 1 in bits 16-31, bit = column), the column control words, the
 // first-iteration magnitudes by check degree.
 struct IlvLds {
-    size_t tsyn, xsyn, xunc, ctl, ctab, bytes;
+    size_t tsyn, xsyn, xunc, ctl, ctab, ring, bytes;
     __host__ __device__ explicit IlvLds(int m) {
         const size_t mw2 = (size_t)(m + 1) / 2;
         tsyn = 0;
@@ -189,7 +197,8 @@ struct IlvLds {
         xunc = 2 * mw2 * 4;
         ctl = (3 * mw2 * 4 + 15) & ~(size_t)15;
         ctab = ctl + (size_t)kIlvCtlWords * 4;
-        bytes = ctab + (size_t)(kFirstTableDeg + 1) * 8;
+        ring = ctab + (size_t)(kFirstTableDeg + 1) * 8;
+        bytes = ring + (size_t)(kIlvBlock / kIlvCols) * 4 * kRingStage * 4;
     }
 };
 
