@@ -59,6 +59,13 @@ constexpr int kCtlMis = 35;       // this round: columns with a check certainly 
 constexpr int kCtlUnc = 36;       // this round: columns with a check whose parity is uncertain
 constexpr int kCtlRefill = 37;    // columns given a new frame (their target syndromes to load)
 constexpr int kCtlIvl = 38;       // columns in an interval iteration (check phase runs)
+constexpr int kCtlDrained = 39;   // the frame queue ran out
+// at most this many columns still iterating once the queue is drained hand
+// their frames off (QKD_ILV_TAIL; 0 keeps every frame to its end)
+#ifndef QKD_ILV_TAIL
+#define QKD_ILV_TAIL 4
+#endif
+constexpr int kIlvTail = QKD_ILV_TAIL;
 
 __device__ __forceinline__ qkds::f2 neg_if(bool neg, qkds::f2 v) {
     return qkds::f2{neg ? -v.y : v.x, neg ? -v.x : v.y};
@@ -128,7 +135,10 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     auto assign = [&](uint32_t need) {
         const uint32_t cnt = (uint32_t)__popc(need);
         uint32_t base = 0;
-        if (lane == 0 && cnt) base = atomicAdd(a.counter, cnt);
+        if (lane == 0 && cnt) {
+            base = atomicAdd(a.counter, cnt);
+            if (base + cnt > a.n_frames) ctl[kCtlDrained] = 1;     // (some columns get no frame)
+        }
         base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
         bool got = false;
         if (lane < kIlvCols && ((need >> lane) & 1u)) {
@@ -517,7 +527,18 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
                     ctl[kCtlIt + lane] = itc + 1;
                 }
             }
-            const uint32_t need = (uint32_t)__ballot(fin) & 0xffffu;
+            uint32_t need = (uint32_t)__ballot(fin) & 0xffffu;
+            // The workgroup's tail: once the queue is drained, a few columns
+            // left iterating would cost whole lockstep rounds (every line is
+            // fetched whatever the number of live columns) and hold the
+            // launch open; their frames go to the split kernel instead
+            // (decoded there from the start, exactly)
+            const uint32_t remain = active & ~need;
+            if (ctl[kCtlDrained] != 0 && remain != 0 && __popc(remain) <= kIlvTail) {
+                if (lane < kIlvCols && ((remain >> lane) & 1u))
+                    a.fb_list[atomicAdd(a.fb_count, 1u)] = ctl[kCtlFrame + lane];
+                need |= remain;
+            }
             if (lane == 0) {
                 ctl[kCtlAbort] = 0;
                 ctl[kCtlKeyMis] = 0;

@@ -180,16 +180,18 @@ def test_interleaved_trials_equal_oracle(Q, big_codes, oracle_mod, monkeypatch, 
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("q,cap", [(0.02, None), (0.03, None), (0.03, "2"), (0.05, None)])
-def test_interleaved_equals_split_at_scale(Q, big_codes, monkeypatch, q, cap):
+@pytest.mark.parametrize("q,cap,frames", [(0.02, None, 4096), (0.03, None, 4096), (0.03, "2", 4096),
+                                          (0.05, None, 4096), (0.04, None, 10000)])
+def test_interleaved_equals_split_at_scale(Q, big_codes, monkeypatch, q, cap, frames):
     """4096 frames: the interleaved decoder (its default for this code at this
     batch size) and the split kernel (QKD_ILV=0) give the same iterations,
     syndrome and key flags. QKD_SPEC_CAP=2 hands every frame still iterating
-    after two interval rounds to the split kernel (its frame-list path)."""
+    after two interval rounds to the split kernel (its frame-list path);
+    10,000 frames take the columns through two to three frames each."""
     H, _ = big_codes
     if cap:
         monkeypatch.setenv("QKD_SPEC_CAP", cap)
-    seeds = torch.from_numpy(Q.make_seeds(2024, 4096).view(np.int64)).cuda()
+    seeds = torch.from_numpy(Q.make_seeds(2024, frames).view(np.int64)).cuda()
     a, b, qq = Q.keygen(H, seeds, q)
     out = {}
     for mode in ("1", "0"):

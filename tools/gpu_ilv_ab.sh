@@ -12,7 +12,7 @@ for l in $LIBS; do
     -k "interleaved" --timeout 200 --timeout-method thread > $O/parity_$l.log 2>&1 || { echo "$l parity failed"; tail -20 $O/parity_$l.log; exit 1; }
   echo "$l parity $(tail -n 1 $O/parity_$l.log)"
 done
-for r in 1 2; do
+for r in $(seq ${REPS:-2}); do
   for l in $LIBS; do
     QKD_ILV=1 QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=$(libpath $l) timeout -k 10 200 python tools/large_code_bench.py --qber 0.02 \
       > $O/lc_$l.json 2> $O/lc_$l.err || { tail $O/lc_$l.err; exit 1; }
