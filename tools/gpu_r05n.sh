@@ -1,4 +1,7 @@
-# Kernel timelines of the long-code bench with the follower on / off.
+# Kernel timelines of the long-code bench with the follower on / off
+# (profiles/r05_ilv_follower_timeline.jsonl). The follower launch was measured
+# slower and removed: QKD_ILV_FOLLOW is no longer read, so
+# both runs of this script now time the same build.
 set -u
 cd "$(dirname "$0")/.."
 O=gpurun_out/r05n
