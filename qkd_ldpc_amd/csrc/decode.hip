@@ -1823,6 +1823,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 af.frame_count = ws->counter + 3;
                 af.spec_cap = 0;
                 af.spec_always = 1;
+                af.phase = nullptr;       // (QKD_PHASE_TIMING: the interleaved kernel's phases)
                 int xdc = 0;
                 DecodeFn ffn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &xdc);
                 if (xdc != sdc)

@@ -182,9 +182,21 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     if (tid < 64) assign((1u << kIlvCols) - 1u);
     __syncthreads();
     refill();
+    // QKD_PHASE_TIMING in a build with -DQKD_ILV_PHASES (thread 0's shader
+    // clock, summed over workgroups): 0 check phase, 1 bit phase, 2 syndrome
+    // test and outcomes, 3 refill. Not in the product build: the clock's
+    // registers live across the frame loop and add spills.
+#ifdef QKD_ILV_PHASES
+    PhaseClock pc(a.phase);
+#else
+    struct {
+        __device__ void mark(int) {}
+    } pc;
+#endif
 
     for (;;) {
         __syncthreads();
+        pc.mark(3);
         const uint32_t active = ctl[kCtlActive];
         if (active == 0) break;
         const uint32_t f = ctl[kCtlFrame + col];
@@ -339,6 +351,7 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
             if (lane == 0 && bm) atomicOr(ctl + kCtlAbort, bm);
         }
         __syncthreads();
+        pc.mark(0);
 
         // ---- bit phase, software-pipelined over the group's bits i, i + G,
         // ...: the next bit's code word, key words and lines are loaded
@@ -475,6 +488,7 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
         }
         if (lane == 0 && kmis) atomicOr(ctl + kCtlKeyMis, kmis);
         __syncthreads();
+        pc.mark(1);
 
         // ---- syndrome test (:285): per column, a check certainly unsatisfied
         // and a check whose parity is uncertain; xsyn / xunc cleared
@@ -553,6 +567,7 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
             if (lane == 0) ctl[kCtlIvl] = ivm;
         }
         __syncthreads();
+        pc.mark(2);
         refill();
     }
 }

@@ -24,13 +24,14 @@ args = ap.parse_args()
 m, cp, ci = regular_code(args.n, seed=11)
 H = Q.HMatrix.from_check_lists(args.n, cp, ci)
 seeds = torch.from_numpy(Q.make_seeds(777, args.frames).view(np.int64)).cuda()
+ws = Q.Workspace(H)
 a, b, q = Q.keygen(H, seeds, args.qber)
-Q.qkd_ldpc(H, a, b, float(q[0]), 50, variant=args.variant)
+Q.qkd_ldpc(H, a, b, float(q[0]), 50, variant=args.variant, workspace=ws)
 torch.cuda.synchronize()
 t = time.perf_counter()
 steps = 5
 for _ in range(steps):
-    r = Q.qkd_ldpc(H, a, b, float(q[0]), 50, variant=args.variant)
+    r = Q.qkd_ldpc(H, a, b, float(q[0]), 50, variant=args.variant, workspace=ws)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t) / steps
 it = r.iterations.cpu().numpy()
@@ -40,7 +41,16 @@ it = r.iterations.cpu().numpy()
 hist = np.bincount(it).tolist()
 lock = {str(g): float(it[: len(it) // g * g].reshape(-1, g).max(axis=1).sum() * g / it[: len(it) // g * g].sum())
         for g in (2, 4, 8, 16)}
-print(json.dumps({"n": args.n, "m": m, "frames": args.frames, "qber": args.qber, "variant": args.variant,
+extra = {}
+if os.environ.get("QKD_PHASE_TIMING"):
+    # the last call's summed shader-clock cycles per phase (the interleaved
+    # decoder: check, bit, syndrome test + outcomes, refill)
+    cyc = np.zeros(7, dtype=np.uint64)
+    Q._native.check(Q._native.lib().qkd_debug_phase_cycles(ws.handle, cyc.ctypes.data))
+    tot = float(cyc.sum())
+    extra["phase_cycles"] = cyc.tolist()
+    extra["phase_share"] = [round(float(x) / tot, 4) for x in cyc] if tot else []
+print(json.dumps({**extra, "n": args.n, "m": m, "frames": args.frames, "qber": args.qber, "variant": args.variant,
                   "ms_per_batch": dt * 1e3, "gbit_s": args.frames * args.n / dt / 1e9,
                   "mean_it": float(it.mean()), "iter_hist": hist, "max_it": int(it.max()),
                   "lockstep_work_ratio": lock, "fer": float(1 - r.keys_match.cpu().numpy().mean())}))
