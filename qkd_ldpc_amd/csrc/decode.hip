@@ -1748,7 +1748,11 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             // in LDS): the frame-interleaved decoder (decode_ilv.hip), its
             // hand-offs decoded by this split kernel from a frame list.
             // QKD_ILV=1 / 0 forces it on / off (tests, A/B).
-            const IlvLds IL(c->m);
+            // (the target syndrome words in LDS when the three arrays fit, else
+            // in global memory: measured 30 % slower at N = 40,000, where
+            // they fit, and twice as fast as the split kernel at 60,000)
+            const bool tsg = IlvLds(c->m, false).bytes > kLdsBytesMax;
+            const IlvLds IL(c->m, tsg);
             bool ilv = mode == kModeKeys && spec && !ckpt && !a.bits_out && a.first_table && c->d_ilv_slots &&
                        IL.bytes <= kLdsBytesMax;
             if (ilv) {
@@ -1758,10 +1762,14 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             }
             DecodeFn ifn = nullptr;
             int igrid = 0;
-            // (per workgroup: the message lines, then the columns' key words)
-            const size_t istride = slots * kIlvCols + (size_t)((c->n + 63) / 64) * kIlvCols * 2;
+            // (per workgroup: the message lines, the columns' key words, their
+            // target syndrome words: (M + 1) / 2 words, in doubles)
+            // rounded to 512 bytes: every workgroup's lines start on a cache
+            // line (an unaligned stride splits each line access in two)
+            const size_t istride = (slots * kIlvCols + (size_t)((c->n + 63) / 64) * kIlvCols * 2 +
+                                    ((size_t)(c->m + 1) / 2 + 1) / 2 + 63) & ~(size_t)63;
             if (ilv) {
-                ifn = pick_ilv(c->ilv_rs, c->max_dc);
+                ifn = pick_ilv(c->ilv_rs, c->max_dc, tsg);
                 QKD_HIP(hipFuncSetAttribute((const void*)ifn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)IL.bytes));
                 int per_cu = 0;
                 QKD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ifn, kIlvBlock, IL.bytes));

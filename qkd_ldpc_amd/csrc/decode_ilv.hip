@@ -79,8 +79,10 @@ __device__ __forceinline__ uint32_t fold_groups(uint64_t b) {
 }  // namespace
 
 // RS: the row stride of DeviceCode::ilv_slots; DM: the largest check degree
-// rounded up to even (the register arrays' size)
-template <int RS, int DM>
+// rounded up to even (the register arrays' size); TG: the target syndrome
+// words in global memory (IlvLds: codes whose three LDS syndrome arrays would
+// not fit)
+template <int RS, int DM, bool TG>
 __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     static_assert(DM <= RS && DM % 2 == 0, "degree bucket");
     using qkds::f2;
@@ -90,9 +92,8 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     const int lane = tid & 63;
     const uint32_t col = (uint32_t)tid & (kIlvCols - 1);
     const int grp = tid / kIlvCols;
-    const IlvLds L(c.m);
+    const IlvLds L(c.m, TG);
     const uint32_t mw2 = (uint32_t)(c.m + 1) >> 1;
-    uint32_t* tsyn = reinterpret_cast<uint32_t*>(smem + L.tsyn);
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
     uint32_t* xunc = reinterpret_cast<uint32_t*>(smem + L.xunc);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
@@ -104,6 +105,13 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     // after the lines: the columns' key words, interleaved ([word][column]
     // {bob, alice}), copied at each refill
     uint4* const keyi = reinterpret_cast<uint4*>(lines + (size_t)c.max_dv * n_pad * kIlvCols);
+    // the columns' target syndrome bits (16 columns x 2 checks per word:
+    // check j is bit ((j & 1) << 4) + column of word j >> 1): in LDS, or (TG)
+    // after the key words in global memory, so the LDS holds only the
+    // syndrome words the bit phase updates (codes up to M ~ 36,000; the check
+    // phase then loads each check's word with its lines)
+    uint32_t* const tsyn = TG ? reinterpret_cast<uint32_t*>(keyi + (size_t)a.words * kIlvCols)
+                              : reinterpret_cast<uint32_t*>(smem + L.tsyn);
     // The lines through a buffer descriptor: a line index of ~0 (an edge past
     // the check's degree, a row past the bit's) gives an offset past the
     // region, which loads 0 and drops the store -- no branch around any
@@ -230,10 +238,20 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
                 const bool ok = grp + t * kIlvGroups < c.m;
                 if (col < (uint32_t)DM) ring[(t & 3) * kRingStage + col] = ok ? r : ~0u;
             };
-            auto lines_issue = [&](int t, double (&v)[DM]) {
+            // check t's lines, and its target syndrome word (a clamped check
+            // index past the last: unused)
+            struct LineSet {
+                double v[DM];
+                uint32_t sw;
+            };
+            auto lines_issue = [&](int t, LineSet& ls) {
                 const uint32_t* st = ring + (t & 3) * kRingStage;
 #pragma unroll
-                for (int k = 0; k < DM; ++k) v[k] = ld_line(part ? st[k] : ~0u);
+                for (int k = 0; k < DM; ++k) ls.v[k] = ld_line(part ? st[k] : ~0u);
+                if constexpr (TG) {
+                    const int jt = grp + t * kIlvGroups;
+                    ls.sw = tsyn[(jt < c.m ? jt : c.m - 1) >> 1];
+                }
             };
             const int nt = (c.m - grp + kIlvGroups - 1) / kIlvGroups;     // this group's checks
             // (memory operations complete in issue order for the waits: each
@@ -244,10 +262,10 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
             idx_commit(1, idx_issue(grp + kIlvGroups));
             idx_commit(2, idx_issue(grp + 2 * kIlvGroups));
             uint32_t rnext = idx_issue(grp + 3 * kIlvGroups);
-            double va[DM], vb[DM];
+            LineSet va, vb;
             lines_issue(0, va);
 #if QKD_ILV_AHEAD == 2
-            double vc[DM];
+            LineSet vc;
             lines_issue(1, vb);
 #endif
             // one check: t's lines in `cur`, t + 1's issued into `ld`. The loop
@@ -257,8 +275,7 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
             // for two checks ahead spills at this occupancy)
             // (rc: the indices of check t + 3, loaded a step earlier; rl: those
             // of check t + 4, loaded now -- two registers alternating, no copy)
-            auto step = [&](int t, const double (&cur)[DM], double (&ld)[DM], const uint32_t& rc,
-                            uint32_t& rl) -> bool {
+            auto step = [&](int t, const LineSet& cur, LineSet& ld, const uint32_t& rc, uint32_t& rl) -> bool {
                 if (t >= nt) return false;
                 const int j = grp + t * kIlvGroups;
                 rl = idx_issue(j + 4 * kIlvGroups);
@@ -274,7 +291,7 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
                 uint32_t negs = 0;
 #pragma unroll
                 for (int k = 0; k < DM; k += 2) {
-                    const f2 b0 = qkds::unpack_iv(cur[k]), b1 = qkds::unpack_iv(cur[k + 1]);
+                    const f2 b0 = qkds::unpack_iv(cur.v[k]), b1 = qkds::unpack_iv(cur.v[k + 1]);
                     const bool n0 = b0.y < 0.0f, n1 = b1.y < 0.0f;
                     const f2 a0 = neg_if(n0, b0), a1 = neg_if(n1, b1);
                     const bool ok0 = a0.x > 1.0e-30f, ok1 = a1.x > 1.0e-30f;
@@ -287,7 +304,7 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
                     ph[k] = (in0 && ok0) ? r0 : f2{0.0f, 0.0f};
                     ph[k + 1] = (in1 && ok1) ? r1 : f2{0.0f, 0.0f};
                 }
-                const uint32_t sbit = (tsyn[j >> 1] >> ((((uint32_t)j & 1u) << 4) + col)) & 1u;
+                const uint32_t sbit = ((TG ? cur.sw : tsyn[j >> 1]) >> ((((uint32_t)j & 1u) << 4) + col)) & 1u;
                 const uint32_t par = (uint32_t)__popc(negs) & 1u;
                 // extrinsic sums over the other edges: prefix sums, then a
                 // backward suffix (every term >= 0, zeros past the degree),
@@ -572,11 +589,16 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     }
 }
 
-DecodeFn pick_ilv(int rs, int max_dc) {
-    if (rs > 8) return decode_ilv_kernel<16, 16>;
-    if (max_dc <= 4) return decode_ilv_kernel<8, 4>;
-    if (max_dc <= 6) return decode_ilv_kernel<8, 6>;
-    return decode_ilv_kernel<8, 8>;
+template <bool TG>
+static DecodeFn pick_ilv_dc(int rs, int max_dc) {
+    if (rs > 8) return decode_ilv_kernel<16, 16, TG>;
+    if (max_dc <= 4) return decode_ilv_kernel<8, 4, TG>;
+    if (max_dc <= 6) return decode_ilv_kernel<8, 6, TG>;
+    return decode_ilv_kernel<8, 8, TG>;
+}
+
+DecodeFn pick_ilv(int rs, int max_dc, bool tsyn_global) {
+    return tsyn_global ? pick_ilv_dc<true>(rs, max_dc) : pick_ilv_dc<false>(rs, max_dc);
 }
 
 }  // namespace qkd

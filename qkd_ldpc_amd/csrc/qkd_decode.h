@@ -190,12 +190,15 @@ constexpr int kRingStage = 16;
 // first-iteration magnitudes by check degree.
 struct IlvLds {
     size_t tsyn, xsyn, xunc, ctl, ctab, ring, bytes;
-    __host__ __device__ explicit IlvLds(int m) {
+    // tsyn_global: the target syndrome words in the workgroup's global region
+    // instead (decode_ilv_kernel's TG), for codes whose three arrays do not fit
+    __host__ __device__ IlvLds(int m, bool tsyn_global) {
         const size_t mw2 = (size_t)(m + 1) / 2;
+        const size_t k = tsyn_global ? 0 : 1;
         tsyn = 0;
-        xsyn = mw2 * 4;
-        xunc = 2 * mw2 * 4;
-        ctl = (3 * mw2 * 4 + 15) & ~(size_t)15;
+        xsyn = k * mw2 * 4;
+        xunc = (k + 1) * mw2 * 4;
+        ctl = ((k + 2) * mw2 * 4 + 15) & ~(size_t)15;
         ctab = ctl + (size_t)kIlvCtlWords * 4;
         ring = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         bytes = ring + (size_t)(kIlvBlock / kIlvCols) * 4 * kRingStage * 4;
@@ -632,7 +635,7 @@ DecodeFn pick_split_decode(int mode, int rule, bool clamp, int max_dc, int* dc);
 // a checkpoint once few checks are unsatisfied).
 DecodeFn pick_split_spec(int mode, int max_dc, bool ckpt, int* dc);
 // the frame-interleaved decoder (decode_ilv.hip) for check-row stride rs (8 or 16)
-DecodeFn pick_ilv(int rs, int max_dc);
+DecodeFn pick_ilv(int rs, int max_dc, bool tsyn_global);
 // decode_split.hip, kModeKeys: the kernels around the split decoder.
 // Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.
 hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream);

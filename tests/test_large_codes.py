@@ -202,3 +202,26 @@ def test_interleaved_equals_split_at_scale(Q, big_codes, monkeypatch, q, cap, fr
     x, y = out["1"], out["0"]
     assert torch.equal(x.iterations, y.iterations)
     assert torch.equal(x.syndromes_match, y.syndromes_match) and torch.equal(x.keys_match, y.keys_match)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [0.02, 0.04])
+def test_interleaved_global_targets_equal_split(Q, monkeypatch, q):
+    """N = 60,000 (M = 30,000): the interleaved decoder's three LDS syndrome
+    arrays would not fit, so its target syndrome words live in global memory
+    (decode_ilv_kernel<..., TG = true>); 1024 frames give the same iterations,
+    syndrome and key flags as the split kernel (QKD_ILV=0)."""
+    n = 60000
+    m, cp, ci = regular_code(n, seed=11)
+    H = Q.HMatrix.from_check_lists(n, cp, ci)
+    seeds = torch.from_numpy(Q.make_seeds(2024, 1024).view(np.int64)).cuda()
+    a, b, qq = Q.keygen(H, seeds, q)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("QKD_ILV", mode)
+        r = Q.qkd_ldpc(H, a, b, float(qq[0]), 50)
+        torch.cuda.synchronize()
+        out[mode] = r
+    x, y = out["1"], out["0"]
+    assert torch.equal(x.iterations, y.iterations)
+    assert torch.equal(x.syndromes_match, y.syndromes_match) and torch.equal(x.keys_match, y.keys_match)
