@@ -287,7 +287,11 @@ QKD_API qkd_status qkd_trace_decode(const qkd_code *code, const double *llr, con
  * the scalar psi_of_exact (11); n even.
  * which = 12 / 13: pairs (x, S) -> (|sign(x) phi(|x|) / ln 2|, phi(S ln 2))
  * of the binary32 variant, from its packed evaluation (12) and from the
- * scalar forms of which = 2 / 3 (13), which must agree bit for bit; n even. */
+ * scalar forms of which = 2 / 3 (13), which must agree bit for bit; n even.
+ * which = 14 / 15: quadruples (a lo, a hi, b lo, b hi) -> the input-form phi
+ * bounds of both intervals from the packed phi_bounds2 (14, the interleaved
+ * decoder's) and two scalar phi_bounds (15); which = 16 / 17 the same for the
+ * output form, phi_bounds_out2 (16) and phi_bounds_out (17); n % 4 == 0. */
 QKD_API qkd_status qkd_debug_math(int which, const double *x, double *y, size_t n, void *stream);
 /* Exhaustive check of the speculative iterations' phi bounds (qkd_spec.h) at
  * EVERY binary32 a with bit pattern in [first_bits, last_bits] (positive

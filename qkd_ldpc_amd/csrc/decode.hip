@@ -1678,10 +1678,18 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             // start off a common alignment (measured: config 2 with the fold table
             // has a region of 13184 slots, 4 % slower than 13248;
             // QKD_C2B_PAD overrides the pad)
-            size_t pad = kC2bPad;
-            if (const char* e = getenv("QKD_C2B_PAD")) pad = (size_t)atol(e);
-            pad = std::min(pad, (size_t)c->n_pad);   // the region stays inside ws_reserve_decode's
-            a.c2b_stride = ((slots - L.S + 31) & ~(size_t)31) + pad;
+            // Default: the region rounded up to an ODD multiple of kC2bPad
+            // slots (512 bytes), so consecutive regions never share an
+            // alignment above 512 bytes (13248 = 207 x 64 is the measured
+            // good case above); QKD_C2B_PAD adds a fixed pad instead.
+            if (const char* e = getenv("QKD_C2B_PAD")) {
+                const size_t pad = std::min((size_t)atol(e), (size_t)c->n_pad);
+                a.c2b_stride = ((slots - L.S + 31) & ~(size_t)31) + pad;
+            } else {
+                size_t st = (slots - L.S + kC2bPad - 1) / kC2bPad;
+                if ((st & 1u) == 0) st++;
+                a.c2b_stride = st * kC2bPad;
+            }
             // an encoded global slot word (kSlotGlobalBase + byte offset) must
             // stay below kSlotLds, the LDS words' tag bit
             if (rule == kRuleSp64 && kSlotGlobalBase + a.c2b_stride * sizeof(double) >= kSlotLds)
@@ -1755,8 +1763,10 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             const IlvLds IL(c->m, tsg);
             bool ilv = mode == kModeKeys && spec && !ckpt && !a.bits_out && a.first_table && c->d_ilv_slots &&
                        IL.bytes <= kLdsBytesMax;
+            bool ilv_forced = false;
             if (ilv) {
                 const char* ie = getenv("QKD_ILV");
+                ilv_forced = ie != nullptr;
                 ilv = ie ? atoi(ie) != 0
                          : (size_t)L.S * 4 < slots && (size_t)a.n_frames * 2 >= (size_t)kIlvCols * c->cu_count;
             }
@@ -1783,11 +1793,21 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                     if (ws->ilv) QKD_HIP(hipFree(ws->ilv));
                     ws->ilv = nullptr;
                     ws->ilv_elems = 0;
-                    if (hipMalloc(&ws->ilv, need * sizeof(double)) != hipSuccess)
-                        return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate %zu B of interleaved "
-                                                                "message lines", need * sizeof(double));
-                    ws->ilv_elems = need;
+                    if (hipMalloc(&ws->ilv, need * sizeof(double)) != hipSuccess) {
+                        // (one message region per resident workgroup: ~6 GB at N
+                        // = 60,000. Unless forced, the split kernel, which needs
+                        // far less, decodes the batch instead)
+                        (void)hipGetLastError();
+                        if (ilv_forced)
+                            return set_error(QKD_ERR_OUT_OF_MEMORY, "workspace: cannot allocate %zu B of "
+                                                                    "interleaved message lines", need * sizeof(double));
+                        ilv = false;
+                    } else {
+                        ws->ilv_elems = need;
+                    }
                 }
+            }
+            if (ilv) {
                 if (ws->fb_frames < a.n_frames) {
                     if (ws->fb_list) QKD_HIP(hipFree(ws->fb_list));
                     ws->fb_list = nullptr;
@@ -1836,18 +1856,19 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 DecodeFn ffn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &xdc);
                 if (xdc != sdc)
                     return set_error(QKD_ERR_UNSUPPORTED, "exact split kernel bucket %d != %d", xdc, sdc);
-                if (hipGetLastError() == hipSuccess)
+                // (the interleaved launch's error is read once and carried to
+                // decoder_event_close: a failed launch skips the hand-offs and
+                // fails the call instead of leaving stale outputs)
+                hipError_t le = hipGetLastError();
+                if (le == hipSuccess) {
                     hipLaunchKernelGGL(ffn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, af);
-                if (getenv("QKD_ILV_STATS")) {      // diagnostic: the hand-off count (synchronises)
-                    uint32_t cnt = 0;
-                    (void)hipStreamSynchronize(stream);
-                    (void)hipMemcpy(&cnt, ws->counter + 3, 4, hipMemcpyDeviceToHost);
-                    fprintf(stderr, "qkd ilv: %u of %u frames handed off\n", cnt, a.n_frames);
+                    le = hipGetLastError();
                 }
+                QKD_HIP(decoder_event_close(ws, stream, le));
             } else {
                 hipLaunchKernelGGL(sfn, dim3(grid), dim3(kDecodeBlock), L.bytes, stream, a);
+                QKD_HIP(decoder_event_close(ws, stream, hipGetLastError()));
             }
-            QKD_HIP(decoder_event_close(ws, stream, hipGetLastError()));
             if (mode == kModeKeys) QKD_HIP(launch_key_match(a, stream));
             return QKD_OK;
         }
@@ -2379,6 +2400,27 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
             y[i + 1] = r.y;
             break;
         }
+        case 14:
+        case 15:
+        case 16:
+        case 17: {
+            // quadruples (a lo, a hi, b lo, b hi) -> the bounds of both
+            // intervals: 14 the packed phi_bounds2, 15 two scalar phi_bounds
+            // (the interleaved decoder's input form); 16 the packed
+            // phi_bounds_out2, 17 two scalar phi_bounds_out (its output form)
+            if (i & 3) break;
+            const qkds::f2 u{(float)x[i], (float)x[i + 1]}, v{(float)x[i + 2], (float)x[i + 3]};
+            qkds::f2 ru, rv;
+            if (which == 14) qkds::phi_bounds2(u, v, ru, rv);
+            else if (which == 16) qkds::phi_bounds_out2(u, v, ru, rv);
+            else if (which == 15) { ru = qkds::phi_bounds(u.x, u.y); rv = qkds::phi_bounds(v.x, v.y); }
+            else { ru = qkds::phi_bounds_out(u.x, u.y); rv = qkds::phi_bounds_out(v.x, v.y); }
+            y[i] = ru.x;
+            y[i + 1] = ru.y;
+            y[i + 2] = rv.x;
+            y[i + 3] = rv.y;
+            break;
+        }
         case 6: y[i] = (double)__builtin_amdgcn_exp2f((float)x[i]); break;   // hardware v_exp_f32
         case 7: y[i] = (double)__builtin_amdgcn_logf((float)x[i]); break;    // hardware v_log_f32
         default: y[i] = (double)RuleMath<kRuleSp32>::two_atanh((float)x[i]); break;  // phi(S ln 2)
@@ -2387,7 +2429,8 @@ __global__ void math_kernel(int which, const double* x, double* y, size_t n) {
 
 qkd_status qkd_debug_math(int which, const double* x, double* y, size_t n, void* stream) {
     clear_error();
-    if (!x || !y || which < 0 || which > 13) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if (!x || !y || which < 0 || which > 17) return set_error(QKD_ERR_INVALID_ARG, "bad argument");
+    if (which >= 14 && (n & 3)) return set_error(QKD_ERR_INVALID_ARG, "packed phi bounds take quadruples");
     if ((which == 10 || which == 11) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "psi pairs take n even");
     if ((which == 12 || which == 13) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "rule pairs take n even");
     if ((which == 4 || which == 5) && (n & 1)) return set_error(QKD_ERR_INVALID_ARG, "phi bounds take pairs (n even)");

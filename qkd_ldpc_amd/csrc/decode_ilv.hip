@@ -543,8 +543,13 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
                 const bool un_c = (ctl[kCtlUnc] >> lane) & 1u;
                 const bool km = (ctl[kCtlKeyMis] >> lane) & 1u;
                 const bool last = itc + 1 >= a.max_it;
+                // (a hand-off for an uncertified round counts as a replay, as
+                // the split kernel's do: the cross-call policy, decode_keys,
+                // and qkd_debug_spec_replays read these counts)
                 if (itc != 0 && (ab || (un_c && (!mi || last)))) {
                     a.fb_list[atomicAdd(a.fb_count, 1u)] = fc;       // to the split kernel
+                    atomicAdd(a.replay_count, 1u);
+                    atomicAdd(a.spec_replays, 1ull);
                     fin = true;
                 } else if (!mi || last) {
                     a.iters[fc] = mi ? a.max_it : itc + 1;
@@ -553,6 +558,8 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
                     fin = true;
                 } else if (itc + 1 >= a.spec_cap) {
                     a.fb_list[atomicAdd(a.fb_count, 1u)] = fc;
+                    atomicAdd(a.replay_count, 1u);
+                    atomicAdd(a.spec_replays, 1ull);
                     fin = true;
                 } else {
                     ctl[kCtlIt + lane] = itc + 1;

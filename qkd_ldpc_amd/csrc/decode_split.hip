@@ -197,15 +197,21 @@ template <> struct BufIo<float> {
 template <typename T, bool ALL = false>
 struct SplitStore {
     T* l;                        // LDS slots [0, S) and the trash slots [S, S + 64)
-    __amdgpu_buffer_rsrc_t g;    // global slots S.. of this workgroup
     uint32_t S;
-    // (for x < S the buffer offset (x - S) * size wraps to at least
-    // 2^32 - S * size, far past the region: out of range without a select)
+    // The global slots S.. of this workgroup: ONE buffer descriptor, gw below
+    // (the check phases' encoded words address it directly; a slot index x >=
+    // S is at byte offset x * size + goff, goff = kSlotGlobalBase - S * size).
+    // One descriptor instead of two: 4 SGPRs fewer in a kernel whose uniform
+    // values already spill to VGPR lanes, read back by v_readlane in the hot
+    // loops (-1.9 % per config-2 batch with the epilogue below, A/B).
+    // (for x < S the offset is kSlotLds: past the descriptor's range, the
+    // load gives 0 and the store is dropped)
+    __device__ __forceinline__ uint32_t gofs(uint32_t x) const { return x * (uint32_t)sizeof(T) + goff; }
     __device__ __forceinline__ T ld(uint32_t x) const {
         if constexpr (ALL) return l[x];
         const bool in = x < S;
         const T vl = l[in ? x : 0u];
-        const T vg = BufIo<T>::ld(g, (x - S) * (uint32_t)sizeof(T));
+        const T vg = BufIo<T>::ld(gw, in ? kSlotLds : gofs(x));
         return in ? vl : vg;
     }
     // The check phases address slots by encoded words (encode_slot,
@@ -217,6 +223,7 @@ struct SplitStore {
     // accesses take the word as it is (the LDS one without its top bit), and
     // a load is the OR of the two halves: no compare, no select.
     __amdgpu_buffer_rsrc_t gw;   // the region, kSlotGlobalBase bytes before its start
+    uint32_t goff;
     // ld_w in two halves for a software pipeline: ld_raw issues both accesses,
     // pick (at the value's first use, a loop iteration later) combines them
     struct Raw {
@@ -249,20 +256,20 @@ struct SplitStore {
         }
         const bool in = x < S;
         l[in ? x : S + (threadIdx.x & 63u)] = v;
-        BufIo<T>::st(g, (x - S) * (uint32_t)sizeof(T), v);
+        BufIo<T>::st(gw, in ? kSlotLds : gofs(x), v);
     }
     // slots x .. x + 63 of a wave's 64 consecutive lanes (xw = the wave's
     // first slot, wave-uniform, a multiple of 64 as S is: SplitLds): all in
     // LDS or all global, one kind of access
     __device__ __forceinline__ T ld_row(uint32_t xw, uint32_t x) const {
         if (ALL || xw < S) return l[x];
-        return BufIo<T>::ld(g, (x - S) * (uint32_t)sizeof(T));
+        return BufIo<T>::ld(gw, gofs(x));
     }
     __device__ __forceinline__ void st_row(uint32_t xw, uint32_t x, T v) const {
         if (ALL || xw < S)
             l[x] = v;
         else
-            BufIo<T>::st(g, (x - S) * (uint32_t)sizeof(T), v);
+            BufIo<T>::st(gw, gofs(x), v);
     }
 };
 
@@ -663,6 +670,12 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
 // whether total <= 0 (the hard decision), each computed with the binary64
 // operations of the per-bit form in the same order (tests/test_spec.py runs
 // both forms).
+// Entry (p, code) sits at position p * 16 + (code ^ (p & 15)): the hot codes
+// (0 and 15: Bob's bit with every message sign agreeing) of the 8 patterns
+// of a (3, 5|6) code would otherwise all fall on two of the eight 32-byte
+// bank groups of an LDS row (iteration 1 measured 0.53 bank-conflict cycles
+// per LDS-active cycle in round 5).
+__device__ __forceinline__ uint32_t fold_tab_pos(uint32_t p, uint32_t code) { return p * 16u + (code ^ (p & 15u)); }
 __device__ void fold_table_fill(const DeviceCode& c, const double* ctab, double log_p, double thr, double* ftab,
                                 int entries) {
     static_assert(kFoldTabPat == 64, "16 codes x 4 entries");
@@ -670,6 +683,7 @@ __device__ void fold_table_fill(const DeviceCode& c, const double* ctab, double 
         const int p = e / kFoldTabPat;
         const uint32_t code = ((uint32_t)e >> 2) & 15u;
         const int k = e & 3;
+        const uint32_t at = fold_tab_pos((uint32_t)p, code) * 4u + (uint32_t)k;
         const uint8_t* degs = c.pat_deg + p * c.max_dv;
         double acc = (code & 1u) ? -log_p : log_p;
         double cv[kDvUnroll];
@@ -690,7 +704,7 @@ __device__ void fold_table_fill(const DeviceCode& c, const double* ctab, double 
             const double ck = k == 0 ? cv[0] : (k == 1 ? cv[1] : cv[2]);
             v = qkds::pack_iv(qkds::psi_of_exact(clamp_msg(acc - ck, thr)));
         }
-        ftab[e] = v;
+        ftab[at] = v;
     }
     __syncthreads();
 }
@@ -750,9 +764,9 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
         const uint32_t x = (uint32_t)k * n_pad + i;
         if constexpr (decltype(fx)::value >= 1) {
             if (k == 0) return ms.l[x];
-            if (k == 2) return BufIo<double>::ld(ms.g, (x - ms.S) * 8u);
+            if (k == 2) return BufIo<double>::ld(ms.gw, ms.gofs(x));
             if constexpr (decltype(fx)::value == 2) return ms.l[x];
-            if constexpr (decltype(fx)::value == 3) return BufIo<double>::ld(ms.g, (x - ms.S) * 8u);
+            if constexpr (decltype(fx)::value == 3) return BufIo<double>::ld(ms.gw, ms.gofs(x));
         }
         return ms.ld_row((uint32_t)k * n_pad + iw, x);
     };
@@ -760,9 +774,9 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
         const uint32_t x = (uint32_t)k * n_pad + i;
         if constexpr (decltype(fx)::value >= 1) {
             if (k == 0) { ms.l[x] = v; return; }
-            if (k == 2) { BufIo<double>::st(ms.g, (x - ms.S) * 8u, v); return; }
+            if (k == 2) { BufIo<double>::st(ms.gw, ms.gofs(x), v); return; }
             if constexpr (decltype(fx)::value == 2) { ms.l[x] = v; return; }
-            if constexpr (decltype(fx)::value == 3) { BufIo<double>::st(ms.g, (x - ms.S) * 8u, v); return; }
+            if constexpr (decltype(fx)::value == 3) { BufIo<double>::st(ms.gw, ms.gofs(x), v); return; }
         }
         ms.st_row((uint32_t)k * n_pad + iw, x, v);
     };
@@ -819,7 +833,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                     const int j = jc[k];
                     code |= (((qsyn[j >> 5] >> (j & 31)) & 1u) ^ sgi) << (1 + k);
                 }
-                const double* e = ftab + (pat[u] * 16u + code) * 4u;
+                const double* e = ftab + fold_tab_pos(pat[u], code) * 4u;
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k) bo[k] = qkds::unpack_iv(e[k]);
                 z = ok && __builtin_bit_cast(unsigned long long, e[kDvUnroll]) != 0ull;
@@ -1011,10 +1025,10 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     T* const region = reinterpret_cast<T*>(a.c2b) + (size_t)region_of_block() * a.c2b_stride;
     const MS ms{
         reinterpret_cast<T*>(smem + L.msg),
-        __builtin_amdgcn_make_buffer_rsrc(region, (short)0, (int)(a.c2b_stride * sizeof(T)), 0x00020000),
         L.S,
         __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(region) - kSlotGlobalBase, (short)0,
-                                          (int)(kSlotGlobalBase + a.c2b_stride * sizeof(T)), 0x00020000)};
+                                          (int)(kSlotGlobalBase + a.c2b_stride * sizeof(T)), 0x00020000),
+        kSlotGlobalBase - L.S * (uint32_t)sizeof(T)};
     // the check phases' plan: encoded slot words for this layout (binary64
     // rule: DecodeArgs::plan_enc, built by the host from L), slot indices for
     // the all-LDS binary32 rule; the dummy column's slot in the same form
@@ -1144,7 +1158,14 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
         const uint64_t* bw = reinterpret_cast<const uint64_t*>(smem + L.tval);
         if (MODE == kModeKeys) {
             uint64_t* w = reinterpret_cast<uint64_t*>(smem + L.tval);
-            for (int q = tid; q < (int)a.words; q += kDecodeBlock) w[q] = a.bob_w[(size_t)f * a.words + q];
+            uint64_t* aw = reinterpret_cast<uint64_t*>(smem + L.aw);
+            const bool ka = a.key_ok != nullptr;
+            for (int q = tid; q < (int)a.words; q += kDecodeBlock) {
+                const uint64_t bv = a.bob_w[(size_t)f * a.words + q];
+                const uint64_t av = ka ? a.alice_w[(size_t)f * a.words + q] : 0ull;
+                w[q] = bv;
+                aw[q] = av;
+            }
             const uint32_t* sy = a.synw + (size_t)f * 2 * m_words;
             for (int q = tid; q < m_words; q += kDecodeBlock) {
                 tsyn[q] = sy[q];
@@ -1192,15 +1213,8 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             for (int q = tid; q < zwords; q += kDecodeBlock)
                 zw[q] = (MODE == kModeKeys && q < (int)a.words) ? bw[q] : 0ull;
             if (MODE == kModeKeys) {
-                for (int w = tid; w < m_words; w += kDecodeBlock) {
-                    uint32_t odd = 0;
-                    if (lsign)
-                        for (int b = 0; b < 32; ++b) {
-                            const int j = w * 32 + b;
-                            odd |= (j < c.m ? (uint32_t)(c.chk_deg[j] & 1u) : 0u) << b;
-                        }
-                    xsyn[w] = tsyn[w] ^ qsyn[w] ^ odd;
-                }
+                for (int w = tid; w < m_words; w += kDecodeBlock)
+                    xsyn[w] = tsyn[w] ^ qsyn[w] ^ (lsign ? c.chk_odd[w] : 0u);
             }
         }
         // ---- prologue, LLR path: target syndrome bits per check (tsyn), thread per check
@@ -1520,18 +1534,14 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 // (Alice's word read here rather than held in registers
                 // through the frame's iterations; both words in the internal
                 // bit order)
+                const uint64_t* aw = reinterpret_cast<const uint64_t*>(smem + L.aw);
                 bool mis = false;
                 if (tid < (int)a.words) {
-                    uint64_t d = zw[tid] ^ a.alice_w[(size_t)f * a.words + tid];
+                    uint64_t d = zw[tid] ^ aw[tid];
                     if ((tid + 1) * 64 > c.n) d &= (1ull << (c.n - tid * 64)) - 1ull;
                     mis = d != 0;
                 }
                 if (__any(mis) && lane == 0) atomicOr(ctl + 7, 1u);
-                __syncthreads();
-                if (tid == 0) {
-                    a.key_ok[f] = ctl[7] ? 0 : 1;
-                    ctl[7] = 0;
-                }
             }
             // the packed decision for bits_out, internal order
             // (zout_unpack_kernel puts the bits back in place)
@@ -1554,6 +1564,10 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             }
         }
         __syncthreads();
+        if (MODE == kModeKeys && a.key_ok && tid == 0) {
+            a.key_ok[f] = ctl[7] ? 0 : 1;
+            ctl[7] = 0;
+        }
     }
     pc.flush();
 }

@@ -47,8 +47,9 @@ static void free_device(qkd_code* c) {
     c->d_bit_code = nullptr;
     if (c->d_pat_deg) (void)hipFree(c->d_pat_deg);
     for (void* p : {(void*)c->d_perm, (void*)c->d_inv, (void*)c->d_bit_chk_s, (void*)c->d_bit_deg_s,
-                    (void*)c->d_bit_pat_s, (void*)c->d_chk_rows16, (void*)c->d_ilv_slots})
+                    (void*)c->d_bit_pat_s, (void*)c->d_chk_rows16, (void*)c->d_ilv_slots, (void*)c->d_chk_odd})
         if (p) (void)hipFree(p);
+    c->d_chk_odd = nullptr;
     c->d_chk_rows16 = nullptr;
     c->chk_rs = 0;
     c->d_ilv_slots = nullptr;
@@ -328,6 +329,14 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     QKD_HIP(hipMemcpy(c->d_chk_bits, chk_bits.data(), chk_bits.size() * sizeof(int32_t),
                       hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_chk_deg, chk_deg.data(), chk_deg.size(), hipMemcpyHostToDevice));
+    {
+        // odd-degree checks as syndrome words (qkd_decode.h decode_m_words)
+        std::vector<uint32_t> odd((size_t)((m + 63) / 64) * 2, 0u);
+        for (int32_t j = 0; j < m; ++j)
+            if (chk_deg[j] & 1u) odd[j >> 5] |= 1u << (j & 31);
+        QKD_HIP(hipMalloc(&c->d_chk_odd, odd.size() * sizeof(uint32_t)));
+        QKD_HIP(hipMemcpy(c->d_chk_odd, odd.data(), odd.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     QKD_HIP(hipMalloc(&c->d_bit_pos, bit_pos.size()));
     QKD_HIP(hipMemcpy(c->d_bit_pos, bit_pos.data(), bit_pos.size(), hipMemcpyHostToDevice));
     QKD_HIP(hipMemcpy(c->d_bit_chk, bit_chk.data(), bit_chk.size() * sizeof(int32_t),

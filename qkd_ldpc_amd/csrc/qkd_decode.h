@@ -548,13 +548,14 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 //   tsyn, xsyn, qsyn [m_words]   target syndrome / XOR-built syndrome / first-product signs
 //   xunc  [m_words]              speculative rounds: checks with an uncertain hard decision
 //   zw    [n_pad / 64] uint64    hard decision of the last bit phase, one bit per bit
+//   aw    [n_words] uint64       keys path: Alice's key words (the epilogue's compare)
 //   tval  [NW][64 + DC] T        per-wave rows for the in-check products
-//                                (prologue: the frame's Alice + Bob words)
+//                                (prologue: the frame's Bob words)
 //   ctab  [kFirstTableDeg + 1]   first-iteration message magnitudes by degree
 //   tab2  [tab2_entries]         second-iteration tanh table
 //   ftab  [ftab_entries]         speculative kernel: the folded first
 //                                iteration's psi bounds and hard decisions
-//   ctl   [8]                    [1] next frame, [4..5] round flags (decode_split.hip)
+//   ctl   [12]                   [1] next frame, [4..5] round flags, [7] key mismatch (decode_split.hip)
 //   wtab  [dc][dc][dc] float     extrinsic-sum weights by (degree, position, k) (dc <= 8)
 //   msg   [S + 64] T             message slots 0 .. S-1 (slots S .. max_dv*n_pad-1
 //                                live in the workgroup's global region), then
@@ -567,7 +568,7 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 __host__ __device__ inline int seg_weight_entries(int dc) { return dc <= 8 ? dc * dc * dc : 0; }
 
 struct SplitLds {
-    size_t tsyn, xsyn, qsyn, xunc, zw, tval, ctab, tab2, ftab, ctl, wtab, msg, bytes;
+    size_t tsyn, xsyn, qsyn, xunc, zw, aw, tval, ctab, tab2, ftab, ctl, wtab, msg, bytes;
     uint32_t S;
     __host__ __device__ SplitLds(int n_pad, int n_words, int m, int max_dv, int dc, int tab2_entries,
                                  int ftab_entries, int esz, size_t budget) {
@@ -577,14 +578,17 @@ struct SplitLds {
         xsyn = qsyn + (size_t)m_words * 4;
         xunc = xsyn + (size_t)m_words * 4;
         zw = (xunc + (size_t)m_words * 4 + 15) & ~(size_t)15;
-        tval = (zw + (size_t)(n_pad / 64) * 8 + 15) & ~(size_t)15;
+        // keys path: Alice's words of the frame, loaded with the prologue's
+        // batch for the epilogue's key compare
+        aw = (zw + (size_t)(n_pad / 64) * 8 + 15) & ~(size_t)15;
+        tval = (aw + (size_t)n_words * 8 + 15) & ~(size_t)15;
         const size_t rows = (size_t)(kDecodeBlock / 64) * (64 + dc) * esz;
-        const size_t stage = (size_t)n_words * 16;
+        const size_t stage = (size_t)n_words * 8;     // (the prologue stages Bob's words there)
         ctab = (tval + (rows > stage ? rows : stage) + 15) & ~(size_t)15;
         tab2 = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         ftab = (tab2 + (size_t)tab2_entries * 8 + 15) & ~(size_t)15;
         ctl = (ftab + (size_t)ftab_entries * 8 + 15) & ~(size_t)15;
-        wtab = ctl + 32;
+        wtab = ctl + 48;
         msg = (wtab + (size_t)seg_weight_entries(dc) * 4 + 15) & ~(size_t)15;
         const size_t slots = (size_t)max_dv * n_pad;
         // 64 trash slots follow the S message slots (decode_split.hip SplitStore)

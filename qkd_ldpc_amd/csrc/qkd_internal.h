@@ -119,6 +119,10 @@ struct DeviceCode {
     // its degree (ilv_rs 8 or 16); nullptr otherwise
     const uint32_t* ilv_slots;
     int32_t ilv_rs;
+    // chk_odd[w] bit b = deg(check 32 w + b) & 1, in the split kernels'
+    // syndrome-word layout (decode_m_words words; the keys path's running
+    // syndrome starts from it, decode_split.hip)
+    const uint32_t* chk_odd;
 };
 
 }  // namespace qkd
@@ -222,6 +226,7 @@ struct qkd_code {
     int32_t chk_rs = 0;
     uint32_t* d_ilv_slots = nullptr;
     int32_t ilv_rs = 0;
+    uint32_t* d_chk_odd = nullptr;
     int32_t* d_bit_chk_s = nullptr;
     uint8_t* d_bit_deg_s = nullptr;
     uint16_t* d_bit_pat_s = nullptr;
@@ -246,14 +251,14 @@ struct qkd_code {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk, d_bit_pos, d_bit_deg,
                                n_pat, d_bit_pat, d_pat_deg, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, 0, nullptr, 0};
+                               nullptr, 0, nullptr, 0, d_chk_odd};
     }
     // the split kernels' view (internal bit order, DeviceCode::perm)
     qkd::DeviceCode view_split() const {
         return qkd::DeviceCode{n, m, e, n_pad, m_pad, max_dv, max_dc, min_dc, min_dv, n_tasks,
                                d_chk_bits, d_chk_deg, d_plan, d_bit_chk_s, nullptr, d_bit_deg_s,
                                n_pat, d_bit_pat_s, d_pat_deg, d_bit_code, d_plan_slot, d_perm, d_inv,
-                               d_chk_rows16, chk_rs, d_ilv_slots, ilv_rs};
+                               d_chk_rows16, chk_rs, d_ilv_slots, ilv_rs, d_chk_odd};
     }
 };
 

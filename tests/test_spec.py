@@ -140,6 +140,45 @@ def test_phi_pair_equals_scalar_forms(Q):
     assert bad.size == 0, (bad[:8], x[bad[:8]], out[8][bad[:8]], out[9][bad[:8]])
 
 
+def _intervals(rng, n, lo_exp, hi_exp, zero_share):
+    lo = np.exp(rng.uniform(np.log(lo_exp), np.log(hi_exp), n)).astype(np.float32)
+    lo[rng.random(n) < zero_share] = 0.0
+    hi = np.maximum(lo, (lo * (1.0 + rng.choice([0.0, 1e-6, 1e-3, 0.3], n)) + 1e-14).astype(np.float32))
+    return lo, hi
+
+
+@pytest.mark.parametrize("packed,scalar,edges", [
+    (14, 15, [0.0, 1e-30, 0.35, 1.0, 2.0, 80.0, 120.0, np.inf]),      # input form (kPhiHuge = 80)
+    (16, 17, [0.0, 1e-12, 0.5, 1.0 / np.log(2), 115.0, 900.0, np.inf]),  # output form (kPsiHuge = 115)
+])
+def test_packed_phi_bounds_equal_scalar(Q, packed, scalar, edges):
+    """The interleaved decoder's packed bound forms (qkds::phi_bounds2 and
+    phi_bounds_out2, decode_ilv.hip's check phase) are bit for bit two scalar
+    phi_bounds / phi_bounds_out, whose soundness the sweeps above establish:
+    1M random interval pairs plus every pair of the forms' branch edges (zero,
+    the clamps kPhiHuge / kPsiHuge, +inf, the x = 1 switch)."""
+    rng = np.random.default_rng(29 + packed)
+    n = 1 << 20
+    alo, ahi = _intervals(rng, n, 1e-30, 1000.0, 0.05)
+    blo, bhi = _intervals(rng, n, 1e-30, 1000.0, 0.05)
+    e = np.array(edges, np.float32)
+    ea, eb = np.meshgrid(e, e)
+    # degenerate intervals at the edges and intervals spanning neighbouring edges
+    k = ea.size
+    alo[:k], ahi[:k] = ea.ravel(), ea.ravel()
+    blo[:k], bhi[:k] = eb.ravel(), np.maximum(eb.ravel(), np.roll(eb.ravel(), 1))
+    x = np.stack([alo, ahi, blo, bhi], axis=1).astype(np.float64).ravel()
+    dx = torch.from_numpy(x).cuda()
+    out = {}
+    for which in (packed, scalar):
+        dy = torch.empty_like(dx)
+        Q._native.check(Q._native.lib().qkd_debug_math(which, dx.data_ptr(), dy.data_ptr(), dx.numel(), None))
+        torch.cuda.synchronize()
+        out[which] = dy.cpu().numpy().astype(np.float32).view(np.uint32)
+    bad = np.nonzero(out[packed] != out[scalar])[0]
+    assert bad.size == 0, (bad[:8], x[bad[:8]], out[packed][bad[:8]], out[scalar][bad[:8]])
+
+
 def test_phi_bounds_out_at_zero(Q):
     """A phi-domain sum that may be 0 (the reference's P / t can be exactly +-1)
     has an infinite upper bound."""
