@@ -78,6 +78,12 @@ def parse():
     ap.add_argument("--config4-frames", type=int, default=None,
                     help="frames of the configs[3] run sharded over the ranks (default 1,000,000, "
                          "0 with --no-sweeps; 0 disables)")
+    ap.add_argument("--phase-timing", action="store_true",
+                    help="per-phase shader-clock shares of the decoder (diagnostic; the QKD_PHASE_TIMING "
+                         "option)")
+    ap.add_argument("--debug-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="a library debug / A-B option (qkd_debug_set_option, include/qkd_ldpc.h), "
+                         "process-wide; repeatable. The library reads no environment variable")
     args = ap.parse_args()
     if args.config4_frames is None:
         args.config4_frames = 0 if args.no_sweeps else 1_000_000
@@ -475,6 +481,9 @@ def main():
         init_rank(world, local)
     import qkd_ldpc_amd as Q
 
+    for kv in args.debug_opt + (["QKD_PHASE_TIMING=1"] if args.phase_timing else []):
+        name, _, value = kv.partition("=")
+        Q.set_debug_option(name, value)
     H, g = load_code(torch.cuda.current_device())
     dev = torch.device("cuda", torch.cuda.current_device())
     from qkd_ldpc_amd.dist import allreduce_counters, imbalance, rank_times, shard_range
@@ -621,7 +630,7 @@ def main():
                 "note": "each rank's own timed loop (before the closing barrier) and its mean decoder "
                         "kernel time (HIP events); imbalance = max / min",
             }
-        if os.environ.get("QKD_PHASE_TIMING"):
+        if args.phase_timing:
             cyc = np.zeros(7, np.uint64)
             Q._native.check(L.qkd_debug_phase_cycles(ws.handle, cyc.ctypes.data))
             names = ["prologue", "check", "bit", "syndrome", "fetch_out", "check_first", "check_second"]

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -50,10 +51,13 @@ void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-int device_index() {
-    const char* d = std::getenv("QKD_AMD_DEVICE");
-    return d ? std::atoi(d) : 0;
-}
+// The device and the decoder variant of the shim's calls: explicit
+// settings (qkd_amd_extensions.hpp), never the environment. Set before the
+// first call (the code cache is per device).
+std::atomic<int> g_device{0};
+std::atomic<uint32_t> g_variant{QKD_VARIANT_SP_F64};
+
+int device_index() { return g_device.load(); }
 
 // ---- code cache ------------------------------------------------------------
 struct CodeKey {
@@ -222,24 +226,8 @@ ThreadCtx& ctx() {
     return *c;
 }
 
-// The reference's only decoder switch is the clamp. QKD_AMD_VARIANT=sp_f32 |
-// minsum | minsum_sc selects one of the library's binary32 variants for a
-// whole run (the
-// default, sp_f64, is the reference's decoder bit for bit).
-uint32_t variant_from_env() {
-    static const uint32_t v = [] {
-        const char* e = std::getenv("QKD_AMD_VARIANT");
-        if (!e || !*e || !std::strcmp(e, "sp_f64")) return QKD_VARIANT_SP_F64;
-        if (!std::strcmp(e, "sp_f32")) return QKD_VARIANT_SP_F32;
-        if (!std::strcmp(e, "minsum")) return QKD_VARIANT_MINSUM;
-        if (!std::strcmp(e, "minsum_sc")) return QKD_VARIANT_MINSUM | QKD_MINSUM_SELF_CORRECT | QKD_MINSUM_SCALE(0.875);
-        throw std::runtime_error(std::string("QKD_AMD_VARIANT: unknown decoder variant '") + e + "'");
-    }();
-    return v;
-}
-
 uint32_t flags_from_cfg() {
-    return (CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD ? QKD_FLAG_THRESHOLD : 0u) | variant_from_env();
+    return (CFG.ENABLE_SUM_PRODUCT_MSG_LLR_THRESHOLD ? QKD_FLAG_THRESHOLD : 0u) | g_variant.load();
 }
 
 // The reference's `while (curr_iteration != max_num_iterations)` runs zero
@@ -323,6 +311,18 @@ const char* kTooSmall = "' is too small for QBER.";
 }  // namespace
 
 // ---- extensions: batched trials ---------------------------------------------
+
+void qkd_amd_set_device(int device) { g_device.store(device); }
+
+void qkd_amd_set_variant(const char* name) {
+    uint32_t v;
+    if (!name || !*name || !std::strcmp(name, "sp_f64")) v = QKD_VARIANT_SP_F64;
+    else if (!std::strcmp(name, "sp_f32")) v = QKD_VARIANT_SP_F32;
+    else if (!std::strcmp(name, "minsum")) v = QKD_VARIANT_MINSUM;
+    else if (!std::strcmp(name, "minsum_sc")) v = QKD_VARIANT_MINSUM | QKD_MINSUM_SELF_CORRECT | QKD_MINSUM_SCALE(0.875);
+    else throw std::runtime_error(std::string("qkd_amd_set_variant: unknown decoder variant '") + name + "'");
+    g_variant.store(v);
+}
 
 std::vector<trial_result> qkd_amd_run_trials(const H_matrix& matrix, double QBER, const size_t* seeds,
                                              size_t count, size_t seed_offset) {

@@ -233,7 +233,35 @@ QKD_API qkd_status qkd_counters_merge(const qkd_counters *records, size_t n_reco
                                       int device, void *stream);
 
 /* ---- diagnostics ------------------------------------------------------------
- * With QKD_PHASE_TIMING set in the environment, decode launches on `ws`
+ * Debug and A/B options. The library reads NO environment variable: every
+ * option defaults to the product behaviour and changes only through this
+ * call. ws != NULL sets the option for that workspace; ws == NULL sets the
+ * process-wide value every workspace uses unless it has its own. value NULL
+ * restores the default. Options (test infrastructure; outputs are bit-exact
+ * under every value unless a variant says otherwise):
+ *   QKD_SPEC_CAP <k>           interval iterations per frame before the exact
+ *                              ones (0: off; default 8)
+ *   QKD_SPEC_CKPT 0|1          force the checkpointed speculation off / on
+ *   QKD_CKPT_UNSAT <k>         its trigger (unsatisfied checks; default 128)
+ *   QKD_SPEC_POLICY always     the in-launch replay policy never turns off
+ *   QKD_FOLD_TABLE 0           the folded first iteration per bit, not tabled
+ *   QKD_DECODE_KERNEL classic  the classic message-store decoder
+ *   QKD_MINSUM_STORE lds|global  the LDS-state / global-store min-sum kernels
+ *   QKD_DECODE_GRID <k>        cap the decoder's resident workgroups
+ *   QKD_SPLIT_BUDGET <bytes>   lower the split decoder's LDS budget
+ *   QKD_C2B_PAD <slots>        a fixed pad of the split decoder's regions
+ *   QKD_ILV 0|1, QKD_ILV_GRID <k>  the interleaved long-code decoder off / on,
+ *                              its workgroup cap
+ *   QKD_KEYGEN serial|replay|lanes|matrix  the other key generators
+ *   QKD_SYN_SLICED 0, QKD_SYN_BYTES 0  the gather frame-syndrome kernel / the
+ *                              separate key packing
+ *   QKD_BIT_ORDER identity|runs  (ws == NULL, read when a code is created)
+ *                              the split decoder's internal bit order
+ *   QKD_PHASE_TIMING 1         per-phase shader clocks (qkd_debug_phase_cycles)
+ * An unknown name fails with QKD_ERR_INVALID_ARG. Thread-safe. No reference
+ * counterpart (the reference's CFG fields are the decode parameters). */
+QKD_API qkd_status qkd_debug_set_option(qkd_workspace *ws, const char *name, const char *value);
+/* With QKD_PHASE_TIMING set (qkd_debug_set_option), decode launches on `ws`
  * accumulate shader-clock cycles per phase, summed over workgroups (thread 0
  * between barriers): [0] per-frame prologue, [1] check phase, [2] bit phase,
  * [3] syndrome test, [4] frame fetch + outputs, [5] / [6] the table-driven
@@ -252,8 +280,8 @@ QKD_API qkd_status qkd_debug_decoder_timing(qkd_workspace *ws, int start, double
  * rule, clamp on) whose speculative interval iterations could not certify a
  * hard decision (or reached the cap) and were decoded again with the exact
  * iterations, accumulated over the launches on `ws` since the last reset;
- * reset != 0 zeroes the count. QKD_SPEC_CAP=<k> in the environment sets how
- * many interval iterations a frame may run first (0: off; default 8).
+ * reset != 0 zeroes the count. The QKD_SPEC_CAP option (qkd_debug_set_option)
+ * sets how many interval iterations a frame may run first (0: off; default 8).
  * Outputs never depend on it. No reference counterpart. */
 QKD_API qkd_status qkd_debug_spec_replays(qkd_workspace *ws, uint64_t *replays, int reset);
 /* Trace of one frame, the reference's TRACE_SUM_PRODUCT / TRACE_SUM_PRODUCT_LLR

@@ -10,7 +10,8 @@ operation rounds exactly as the kernel's does:
   b2c           LLR_i at iteration 0 (:188), else clamp(total_i - c2b) (:303-316)
   c2b           (-1)^(s_j + #negative other b2c) * max(scale * min over the other
                 |b2c| - offset, 0) (offset 0: plain normalised min-sum; NaN inputs
-                ignored by the min, as fminf), then clamp (:246-249)
+                ignored by the min, as fminf, which is +inf when no other edge
+                has a number), then clamp (:246-249)
   self-correct  (QKD_MINSUM_SELF_CORRECT, Savin's self-corrected min-sum) from the
                 second iteration on, a b2c whose sign differs from the edge's
                 previous b2c, both nonzero, is erased to 0 before the check rule
@@ -94,7 +95,8 @@ class MinSumModel:
             new = np.zeros_like(c2b)
             for k in range(self.dc):
                 others = np.delete(mag, k, axis=2)
-                mn = np.fmin.reduce(others, axis=2) if others.shape[2] else np.full(mag.shape[:2], np.inf, np.float32)
+                # (NaN magnitudes ignored, as fminf; +inf when no other edge has a number)
+                mn = np.fmin.reduce(others, axis=2, initial=np.inf) if others.shape[2] else np.full(mag.shape[:2], np.inf, np.float32)
                 mn = mn.astype(np.float32)
                 v = (sc * mn).astype(np.float32)
                 if offset > 0:

@@ -39,7 +39,7 @@ __all__ = [
     "HMatrix", "QkdError", "calculate_syndrome", "sum_product_decoding",
     "sum_product_decoding_irregular", "sum_product_decoding_regular", "qkd_ldpc",
     "QKD_LDPC_irregular", "QKD_LDPC_regular", "keygen", "run_trials", "make_seeds",
-    "qber_range", "Workspace", "counters_to_stats", "decoder_flags", "trace_decode",
+    "qber_range", "Workspace", "counters_to_stats", "decoder_flags", "trace_decode", "set_debug_option",
     "spec_replays", "interactive_simulation",
 ]
 
@@ -228,6 +228,14 @@ class Workspace:
 
 def _ws(ws):
     return ws.handle if ws is not None else None
+
+
+def set_debug_option(name: str, value=None, workspace: "Workspace | None" = None) -> None:
+    """qkd_debug_set_option: a debug / A-B option (include/qkd_ldpc.h lists
+    them) for `workspace`, or process-wide when None; value None restores the
+    default (the product behaviour). The library reads no environment variable."""
+    v = None if value is None else str(value).encode()
+    N.check(N.lib().qkd_debug_set_option(_ws(workspace), name.encode(), v))
 
 
 def spec_replays(ws: Workspace, reset: bool = False) -> int:

@@ -64,7 +64,7 @@ EXPORTS = [
     "qkd_qber_range", "qkd_debug_phase_cycles", "qkd_debug_spec_replays", "qkd_debug_math", "qkd_debug_phi_sweep", "qkd_trace_decode",
     "qkd_interactive_batch",
     "qkd_code_from_alist_ex", "qkd_debug_decoder_timing", "qkd_debug_bit_order",
-    "qkd_counters_merge",
+    "qkd_counters_merge", "qkd_debug_set_option",
 ]
 
 
@@ -133,6 +133,7 @@ def lib():
             "qkd_debug_math": (st, [C.c_int, P, P, SZ, P]),
             "qkd_debug_phi_sweep": (st, [C.c_int, C.c_uint32, C.c_uint32, P]),
             "qkd_debug_bit_order": (st, [I32, I32, P, P, C.c_char_p, P, P, C.POINTER(I32)]),
+            "qkd_debug_set_option": (st, [P, C.c_char_p, C.c_char_p]),
             "qkd_interactive_batch": (st, [P, P, C.c_uint64, SZ, P, C.c_uint32, C.c_double, C.c_uint32,
                                            P, P, P, P, P, P]),
             "qkd_trace_decode": (st, [P, P, P, U32, D, U32, P, P, P, P]),

@@ -1563,15 +1563,17 @@ static hipError_t decoder_event_close(qkd_workspace* ws, hipStream_t stream, hip
 // DeviceCode::plan_slot encoded for a split-kernel layout and check-degree
 // bucket: slot words by encode_slot (binary64 slots), segment words by
 // encode_seg; built on a layout's first launch and kept with the code
-static qkd_status plan_for_layout(const qkd_code* c, const SplitLds& L, int dc, const uint2** out) {
+// esz 4 (the binary32 min-sum rules, every slot in LDS): the slot word is
+// the slot's LDS byte address itself (no kSlotLds tag, no global form)
+static qkd_status plan_for_layout(const qkd_code* c, const SplitLds& L, int dc, const uint2** out, int esz = 8) {
     std::lock_guard<std::mutex> lock(c->plan_mu);
-    const auto key = std::make_pair(L.S, ((uint32_t)L.msg << 8) | (uint32_t)dc);
+    const auto key = std::make_pair(L.S, ((uint32_t)L.msg << 8) | (uint32_t)dc | (esz == 4 ? 0x80u : 0u));
     auto it = c->d_plan_enc.find(key);
     if (it == c->d_plan_enc.end()) {
         std::vector<uint2> enc(c->plan_slot_host);
         for (size_t k = 0; k < enc.size(); ++k) {
             uint2& w = enc[k];
-            w.x = encode_slot(w.x, L.S, (uint32_t)L.msg, (uint32_t)sizeof(double));
+            w.x = esz == 4 ? (uint32_t)L.msg + w.x * 4u : encode_slot(w.x, L.S, (uint32_t)L.msg, (uint32_t)sizeof(double));
             w.y = encode_seg(w.y & qkdp::kPlanChkMask, (w.y >> 20) & 63u, (w.y >> 26) + 1, (uint32_t)(k & 63),
                              (uint32_t)dc);
         }
@@ -1613,30 +1615,43 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     int dc = 0;
     int rule = rule_of(flags);
     // QKD_MINSUM_STORE=global keeps the global-message-store min-sum (tests)
-    const char* ms_store = getenv("QKD_MINSUM_STORE");
-    const bool ms_global = ms_store && !strcmp(ms_store, "global");
+    // (QKD_MINSUM_STORE=lds keeps the LDS-state kernel: tests)
+    const DbgOpt ms_store = debug_option(ws, "QKD_MINSUM_STORE");
+    const bool ms_global = ms_store.is("global");
+    const bool ms_lds = ms_store.is("lds");
     a.ms_sc = (flags & QKD_MINSUM_SELF_CORRECT) ? 1 : 0;
+    const bool classic = debug_option(ws, "QKD_DECODE_KERNEL").is("classic");
+    // min-sum: the split skeleton (every binary32 slot in LDS, the binary32
+    // rule's bit phase over DeviceCode::bit_code) when it applies, else the
+    // LDS-state kernel, else the global message store
+    if (rule == kRuleMinSum && !ms_global && !ms_lds && !classic && !a.trace && c->d_bit_code &&
+        c->n <= kMaxBitsSplit && c->m <= kMaxChecksSplit && c->max_dc <= 8) {
+        // (check degree <= 8: the additive mask table, seg_weight_entries)
+        const SplitLds Lm(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, c->max_dc <= 4 ? 4 : c->max_dc <= 6 ? 6 : 8,
+                          0, a.ms_sc ? 2 * c->n_tasks : 0, 4, kLdsBytesMax);
+        if (Lm.S >= (uint32_t)((size_t)c->max_dv * c->n_pad) && Lm.bytes <= kLdsBytesMax)
+            rule = a.ms_sc ? kRuleMinSumSplitSc : kRuleMinSumSplit;
+    }
     if (rule == kRuleMinSum && !ms_global && decode_ms_fits(c, a.ms_sc != 0)) rule = kRuleMinSumLds;
-    if (a.ms_sc && rule != kRuleMinSumLds)
-        return set_error(QKD_ERR_UNSUPPORTED, "self-corrected min-sum needs the LDS-state min-sum kernel "
-                                              "(check degree <= 32, its state in LDS)");
-    if (a.ms_sc) rule = kRuleMinSumLdsSc;
+    if (a.ms_sc && rule != kRuleMinSumLds && rule != kRuleMinSumSplitSc)
+        return set_error(QKD_ERR_UNSUPPORTED, "self-corrected min-sum needs the split or the LDS-state min-sum "
+                                              "kernel (check degree <= 32, its state in LDS)");
+    if (a.ms_sc && rule == kRuleMinSumLds) rule = kRuleMinSumLdsSc;
     a.ms_scale = minsum_scale_of(flags);
     a.ms_offset = (float)((flags >> QKD_MINSUM_OFFSET_SHIFT) & 0xffu) / 64.0f;
     // The split-store kernel (decode_split.hip) for the sum-product rules
     // whenever its LDS layout fits; QKD_DECODE_KERNEL=classic keeps
     // decode_kernel (A/B measurements, tests). Trace mode records the classic
     // kernel's store.
-    const char* kern = getenv("QKD_DECODE_KERNEL");
-    const bool classic = kern && !strcmp(kern, "classic");
-    if ((rule == kRuleSp64 || rule == kRuleSp32) && !classic && !a.trace && c->n <= kMaxBitsSplit &&
+    const bool msr = rule == kRuleMinSumSplit || rule == kRuleMinSumSplitSc;
+    if ((rule == kRuleSp64 || rule == kRuleSp32 || msr) && !classic && !a.trace && c->n <= kMaxBitsSplit &&
         c->m <= kMaxChecksSplit) {
         int sdc = 0;
         DecodeFn sfn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &sdc);
         const int esz = rule == kRuleSp64 ? 8 : 4;
         // diagnostic: QKD_SPLIT_BUDGET lowers the LDS budget (fewer LDS slots)
         size_t budget = kLdsBytesMax;
-        if (const char* b = getenv("QKD_SPLIT_BUDGET")) budget = std::min(budget, (size_t)atol(b));
+        if (const DbgOpt b = debug_option(ws, "QKD_SPLIT_BUDGET")) budget = std::min(budget, (size_t)b.as_long());
         // the speculative kernel (interval iterations, qkd_spec.h, exact
         // replays in place) when it applies: QKD path with the folded first
         // iteration, binary64 rule, clamped messages, bit degree <= kDvUnroll
@@ -1650,27 +1665,29 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                           c->n_pat * kFoldTabPat <= kFoldTabMaxEntries)
                              ? c->n_pat * kFoldTabPat : 0;
         // (QKD_FOLD_TABLE=0: the per-bit form; tests compare the two)
-        if (const char* e = getenv("QKD_FOLD_TABLE")) if (atoi(e) == 0) a.ftab_entries = 0;
-        if (const char* e = getenv("QKD_SPEC_POLICY")) a.spec_always = strcmp(e, "always") == 0 ? 1u : 0u;
+        if (const DbgOpt e = debug_option(ws, "QKD_FOLD_TABLE")) if (e.as_int() == 0) a.ftab_entries = 0;
+        if (debug_option(ws, "QKD_SPEC_POLICY").is("always")) a.spec_always = 1u;
+        // (self-corrected min-sum: its previous-b2c ballot words in the ftab region)
+        if (rule == kRuleMinSumSplitSc) a.ftab_entries = 2 * c->n_tasks;
         const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, a.ftab_entries, esz,
                          budget);
         // (the binary32 rule's kernel keeps every slot in LDS: SplitStore<float, true>)
         // (binary64: any share of the slots in LDS, the rest in the
         // workgroup's global region; long codes keep most of them there)
-        const bool fits = rule == kRuleSp32 ? L.S >= (uint32_t)((size_t)c->max_dv * c->n_pad) : L.S >= 64;
+        const bool fits = rule != kRuleSp64 ? L.S >= (uint32_t)((size_t)c->max_dv * c->n_pad) : L.S >= 64;
         if (L.bytes <= kLdsBytesMax && fits) {
             int grid = 0;
             qkd_status s = decode_grid(c, sfn, L.bytes, &grid);
             if (s != QKD_OK) return s;
             grid = (int)std::min<size_t>((size_t)grid, a.n_frames);
-            if (const char* g = getenv("QKD_DECODE_GRID")) grid = std::max(1, std::min(grid, atoi(g)));
+            if (const DbgOpt g = debug_option(ws, "QKD_DECODE_GRID")) grid = std::max(1, std::min(grid, g.as_int()));
             s = ws_reserve_decode(ws, (size_t)grid);
             if (s != QKD_OK) return s;
             a.code = c->view_split();     // the internal bit order (host.cpp build_code)
             a.c2b = ws->c2b;
             a.plan_enc = nullptr;
-            if (rule == kRuleSp64) {
-                s = plan_for_layout(c, L, sdc, &a.plan_enc);
+            if (rule == kRuleSp64 || msr) {
+                s = plan_for_layout(c, L, sdc, &a.plan_enc, esz);
                 if (s != QKD_OK) return s;
             }
             const size_t slots = (size_t)c->max_dv * c->n_pad;
@@ -1682,8 +1699,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             // slots (512 bytes), so consecutive regions never share an
             // alignment above 512 bytes (13248 = 207 x 64 is the measured
             // good case above); QKD_C2B_PAD adds a fixed pad instead.
-            if (const char* e = getenv("QKD_C2B_PAD")) {
-                const size_t pad = std::min((size_t)atol(e), (size_t)c->n_pad);
+            if (const DbgOpt e = debug_option(ws, "QKD_C2B_PAD")) {
+                const size_t pad = std::min((size_t)e.as_long(), (size_t)c->n_pad);
                 a.c2b_stride = ((slots - L.S + 31) & ~(size_t)31) + pad;
             } else {
                 size_t st = (slots - L.S + kC2bPad - 1) / kC2bPad;
@@ -1697,7 +1714,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                                                       "(%zu global slots per frame)", a.c2b_stride);
             a.lds_budget = (uint32_t)budget;
             a.counter = ws->counter;
-            static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;
+            const bool timing = (bool)debug_option(ws, "QKD_PHASE_TIMING");
             a.phase = nullptr;
             if (timing) {
                 a.phase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 64);
@@ -1748,7 +1765,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 }
                 a.win = ws->win;
             }
-            if (rule == kRuleSp64) {
+            if (rule == kRuleSp64 || msr) {
                 s = check_no_static_lds(sfn);
                 if (s != QKD_OK) return s;
             }
@@ -1765,9 +1782,9 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                        IL.bytes <= kLdsBytesMax;
             bool ilv_forced = false;
             if (ilv) {
-                const char* ie = getenv("QKD_ILV");
-                ilv_forced = ie != nullptr;
-                ilv = ie ? atoi(ie) != 0
+                const DbgOpt ie = debug_option(ws, "QKD_ILV");
+                ilv_forced = (bool)ie;
+                ilv = ie ? ie.as_int() != 0
                          : (size_t)L.S * 4 < slots && (size_t)a.n_frames * 2 >= (size_t)kIlvCols * c->cu_count;
             }
             DecodeFn ifn = nullptr;
@@ -1787,7 +1804,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 igrid = per_cu * c->cu_count;
                 igrid = (int)std::min<size_t>((size_t)igrid, ((size_t)a.n_frames + kIlvCols - 1) / kIlvCols);
                 // (QKD_ILV_GRID caps the workgroups: tests take columns through several frames)
-                if (const char* g = getenv("QKD_ILV_GRID")) igrid = std::max(1, std::min(igrid, atoi(g)));
+                if (const DbgOpt g = debug_option(ws, "QKD_ILV_GRID")) igrid = std::max(1, std::min(igrid, g.as_int()));
                 const size_t need = (size_t)igrid * istride;
                 if (ws->ilv_elems < need) {
                     if (ws->ilv) QKD_HIP(hipFree(ws->ilv));
@@ -1827,7 +1844,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             if (mode == kModeKeys) {
                 a.synw = ws->synw;
                 a.zout = ws->zout;
-                QKD_HIP(launch_frame_syn(a, stream));
+                QKD_HIP(launch_frame_syn(a, stream, debug_option(ws, "QKD_SYN_SLICED").is("0"),
+                                         debug_option(ws, "QKD_SYN_BYTES").is("0")));
             } else {
                 QKD_HIP(hipMemsetAsync(ws->counter, 0, 8, stream));
                 if (a.win) QKD_HIP(hipMemsetAsync(a.win, 0, 2 * (size_t)a.win_count * sizeof(uint32_t), stream));
@@ -1885,7 +1903,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     if (s != QKD_OK) return s;
     grid = (int)std::min<size_t>((size_t)grid, a.n_frames);
     // diagnostic: QKD_DECODE_GRID caps the resident workgroups (frames in flight)
-    if (const char* g = getenv("QKD_DECODE_GRID")) grid = std::max(1, std::min(grid, atoi(g)));
+    if (const DbgOpt g = debug_option(ws, "QKD_DECODE_GRID")) grid = std::max(1, std::min(grid, g.as_int()));
     s = ws_reserve_decode(ws, (rule == kRuleMinSumLds || rule == kRuleMinSumLdsSc) ? 0 : (size_t)grid);   // no global messages
     if (s != QKD_OK) return s;
     a.code = c->view();
@@ -1898,7 +1916,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     a.totals_stride = c->n_pad;
     a.counter = ws->counter;
     QKD_HIP(hipMemsetAsync(ws->counter, 0, 4, stream));
-    static const bool timing = getenv("QKD_PHASE_TIMING") != nullptr;
+    const bool timing = (bool)debug_option(ws, "QKD_PHASE_TIMING");
     a.phase = nullptr;
     if (timing) {
         a.phase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 64);
@@ -2009,7 +2027,7 @@ qkd_status qkd_decode_batch(const qkd_code* c, qkd_workspace* ws, const double* 
     // speculative interval iterations (decode_split.hip, qkd_spec.h): binary64
     // rule with clamped messages; QKD_SPEC_CAP overrides how many (0: off)
     int cap = kSpecCapDefault;
-    if (const char* e = getenv("QKD_SPEC_CAP")) cap = std::max(0, atoi(e));
+    if (const DbgOpt e = debug_option(ws, "QKD_SPEC_CAP")) cap = std::max(0, e.as_int());
     a.spec_cap = (rule_of(flags) == kRuleSp64 && a.clamp_on) ? (uint32_t)cap : 0u;
     a.thr_dn = f32_bound(msg_threshold, false);
     a.thr_up = f32_bound(msg_threshold, true);
@@ -2047,8 +2065,12 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     // first-iteration message magnitudes by check degree (first_check_phase)
     // (the binary32 rule folds on the device, decode_split_kernel; not at
     // log_p = 0, where Bob's 1 bits give -0.0, not negative)
+    // (min-sum folds on the device too, decode_split_kernel, without the
+    // self-correction, whose first check phase records every b2c)
     a.first_table = (c->max_dc <= kFirstTableDeg &&
-                     (rule_of(flags) == kRuleSp64 || (rule_of(flags) == kRuleSp32 && a.log_p != 0.0))) ? 1 : 0;
+                     (rule_of(flags) == kRuleSp64 || (rule_of(flags) == kRuleSp32 && a.log_p != 0.0) ||
+                      (rule_of(flags) == kRuleMinSum && !(flags & QKD_MINSUM_SELF_CORRECT) && a.log_p != 0.0)))
+                        ? 1 : 0;
     if (a.first_table) {
         const double T = std::fabs(qkdm::tanh_flat(a.log_p / 2.0));
         double M = 1.0;
@@ -2066,7 +2088,7 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     // the exact ones, for the binary64 rule with clamped messages;
     // QKD_SPEC_CAP overrides how many (0: off)
     int cap = kSpecCapDefault;
-    if (const char* e = getenv("QKD_SPEC_CAP")) cap = std::max(0, atoi(e));
+    if (const DbgOpt e = debug_option(ws, "QKD_SPEC_CAP")) cap = std::max(0, e.as_int());
     a.spec_cap = (rule_of(flags) == kRuleSp64 && a.clamp_on && a.first_table) ? (uint32_t)cap : 0u;
     a.lp_dn = f32_bound(a.log_p, false);
     a.lp_up = f32_bound(a.log_p, true);
@@ -2092,10 +2114,10 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     a.ckpt_stride = 0;
     a.ckpt_unsat = 0;
     // (QKD_SPEC_CKPT=1: the checkpointed variant at every QBER; tests)
-    const char* force_ck = getenv("QKD_SPEC_CKPT");
-    if (q >= ws->spec_ckpt_q || (force_ck && atoi(force_ck) == 1)) {
+    const DbgOpt force_ck = debug_option(ws, "QKD_SPEC_CKPT");
+    if (q >= ws->spec_ckpt_q || (force_ck && force_ck.as_int() == 1)) {
         int cu = kCkptUnsatDefault;
-        if (const char* e = getenv("QKD_CKPT_UNSAT")) cu = std::max(0, atoi(e));
+        if (const DbgOpt e = debug_option(ws, "QKD_CKPT_UNSAT")) cu = std::max(0, e.as_int());
         a.ckpt_unsat = (uint32_t)cu;
         if (cu == 0) a.spec_cap = 0;
     }
@@ -2160,11 +2182,11 @@ static qkd_status keygen_into_ws(const qkd_code* c, qkd_workspace* ws, const uin
     // the two-wave kernel's serial path for every frame, QKD_KEYGEN=lanes the
     // one-wave kernel (keygen_fast_kernel), QKD_KEYGEN=matrix that kernel with its
     // lane jumps as GF(2) matrix products instead of polynomials (tests of all).
-    const char* mode = getenv("QKD_KEYGEN");
-    const bool serial = mode && !strcmp(mode, "serial");
-    const uint32_t replay = mode && !strcmp(mode, "replay") ? 1u : 0u;
-    const bool matrix = mode && !strcmp(mode, "matrix");
-    const bool lanes = mode && !strcmp(mode, "lanes");
+    const DbgOpt mode = debug_option(ws, "QKD_KEYGEN");
+    const bool serial = mode.is("serial");
+    const uint32_t replay = mode.is("replay") ? 1u : 0u;
+    const bool matrix = mode.is("matrix");
+    const bool lanes = mode.is("lanes");
     // the two-wave generator (default; QKD_KEYGEN=replay forces its serial path)
     const size_t lds2 = (size_t)kKgSplitFrames * ((2 * (size_t)ne + 2 * (ne / 2 + 1)) * sizeof(uint32_t) +
                                                   2 * (size_t)words * sizeof(uint64_t));

@@ -385,40 +385,148 @@ __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan,
     }
 }
 
+// ---- min-sum on the split skeleton (kRuleMinSumSplit / kRuleMinSumSplitSc) --
+// The binary32 rules' all-LDS store (4 bytes per edge, SplitStore<float,
+// true>) and their bit phase (sp32_bit_phase); the check phase per edge
+// (the min-sum specification tests/test_variants.py checks, bit for bit):
+//   c2b = (-1)^(s_j + #negative other b2c) * max(scale * min |other b2c| - off, 0),
+//   clamped (:246-249)
+// The extrinsic min reads the task's row of |b2c| through an additive mask
+// table (mtab: 0 for the segment's other lanes, +inf for this lane and past
+// the segment), so it is one add and one min per row entry (v_min3 pairs),
+// NaN magnitudes ignored as fminf does; the sign is the segment parity of one
+// ballot, as sp32_check_phase's.
+// SC (Savin's self-correction, QKD_MINSUM_SELF_CORRECT): a b2c whose sign
+// differs from the edge's previous b2c, both nonzero, is erased to 0 before
+// the rule. The previous b2c of every edge is two ballot words per task in
+// LDS (scw[2 t]: negative, scw[2 t + 1]: nonzero), read and rewritten by the
+// task's wave; sc_on is false in the frame's first check phase (no previous).
+template <bool CLAMP, int DC, bool SC, bool OFF, typename MS>
+__device__ __forceinline__ void ms_split_check_phase(const uint2* __restrict__ plan, const MS& ms, float* row,
+                                                     const float* mtab, uint64_t* scw, bool sc_on, int n_tasks,
+                                                     float thr, float scale, float off, int wave, int lane) {
+    static_assert(DC <= 8, "min-sum split buckets: check degree <= 8 (the mask table)");
+    typedef __attribute__((address_space(3))) float LdsF;
+    constexpr int NW = kDecodeBlock / 64;
+    int t = wave;
+    if (t >= n_tasks) return;
+    const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
+    // (entries past lane 63 are read by segments ending there, masked: finite)
+    if (lane < DC) row[64 + lane] = 0.0f;
+    // the plan is encoded for this layout (plan_for_layout, binary32): the
+    // slot's LDS byte address, and encode_seg's pre-decoded segment fields
+    auto slot = [](uint2 p) -> LdsF* { return reinterpret_cast<LdsF*>((size_t)p.x); };
+    // b2c of task tt's edge after the self-correction; records it as the
+    // edge's previous b2c
+    auto input = [&](float x, int tt) -> float {
+        if constexpr (SC) {
+            if (sc_on) {
+                const uint64_t pneg = scw[2 * tt], pnz = scw[2 * tt + 1];
+                const bool er = ((pnz >> lane) & 1ull) && x != 0.0f && (x < 0.0f) != (((pneg >> lane) & 1ull) != 0);
+                x = er ? 0.0f : x;
+            }
+            const uint64_t nneg = __ballot(x < 0.0f), nnz = __ballot(x != 0.0f);
+            if (lane == 0) {
+                scw[2 * tt] = nneg;
+                scw[2 * tt + 1] = nnz;
+            }
+        }
+        return x;
+    };
+    uint2 wt = plan_word(prs, t, lane);
+    uint2 wn = plan_word(prs, t + NW, lane);
+    uint2 wnn = plan_word(prs, t + 2 * NW, lane);
+    float xt = input(*slot(wt), t);
+    row[lane] = __builtin_fabsf(xt);
+    uint64_t sgn_t = __ballot(xt < 0.0f);
+    bool neg_t = xt < 0.0f;
+    // One task: task t's c2b from the row, then task t + NW's row entry from
+    // its slot (read a task earlier); loads the plan word three tasks ahead
+    // (w_ld) and the slot of task t + 2 NW (x_ld). Unrolled four times over
+    // rotating registers: no copies, so no load is waited for early.
+    auto step = [&](const uint2 w_t, const uint2 w_n, const uint2 w_nn, uint2& w_ld, const float x_n,
+                    float& x_ld) -> bool {
+        w_ld = plan_word(prs, t + 3 * NW, lane);
+        x_ld = *slot(w_nn);
+        wave_lds_sync();
+        const int start = seg_start(w_t);
+        const float* mk = mtab + seg_wi(w_t) * DC;
+        float mn = __builtin_inff();
+#pragma unroll
+        for (int k = 0; k < DC; ++k) mn = __builtin_fminf(mn, row[start + k] + mk[k]);
+        float v = scale * mn;
+        if constexpr (OFF) v = __builtin_fmaxf(v - off, 0.0f);
+        const uint32_t neg = seg_sbit(w_t) ^ seg_parity_enc<DC>(sgn_t, w_t) ^ (neg_t ? 1u : 0u);
+        // v >= +0 is never NaN (the chain starts at +inf), so clamp_msg of +-v
+        // is +-med3(v, 0, thr)
+        const float m = CLAMP ? __builtin_amdgcn_fmed3f(v, 0.0f, thr) : v;
+        *slot(w_t) = neg ? -m : m;
+        t += NW;
+        if (t >= n_tasks) return false;
+        // the next task's row (after this task's row reads: a wave's LDS
+        // accesses complete in order)
+        const float xc = input(x_n, t);
+        row[lane] = __builtin_fabsf(xc);
+        sgn_t = __ballot(xc < 0.0f);
+        neg_t = xc < 0.0f;
+        return true;
+    };
+    float xa = *slot(wn), xb;
+    uint2 wd;
+    for (;;) {
+        if (!step(wt, wn, wnn, wd, xa, xb)) break;
+        if (!step(wn, wnn, wd, wt, xb, xa)) break;
+        if (!step(wnn, wd, wt, wn, xa, xb)) break;
+        if (!step(wd, wt, wn, wnn, xb, xa)) break;
+    }
+}
+
 // Bit phase of the binary32 rule over DeviceCode::bit_code (one load per bit
 // for its checks and their degrees): total = LLR + c2b_0 + c2b_1 + ...
 // ascending (:256-267), the hard decision and its syndrome, b2c_k =
 // clamp(total - c2b_k) (:303-316); FOLD: the first iteration's messages
 // +-C_d (fold_first_message). The operations of the generic bit phase.
 constexpr int kSp32Chunk = 3;     // bit-phase rounds per load batch
-template <bool FOLD, int MODE, bool CLAMP, typename MS>
+static_assert(kSp32Chunk - 1 <= kBitPadRounds, "per-bit arrays padded past the last load batch (host.cpp)");
+// DV3: every bit has exactly kDvUnroll (3) checks (the reference's N = 10240
+// code): no per-row degree guards, so a round's loads, sums and stores are
+// straight-line code (the guarded form compiled each row's store to an
+// exec-mask branch; the min-sum rule spends 40 % of its time here). Whole
+// batches of full rounds skip the per-round bounds tests (as spec_bit_phase).
+template <bool FOLD, int MODE, bool CLAMP, bool DV3, typename MS>
 __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const DecodeArgs& a, const MS& ms,
                                                const uint32_t* qsyn, const double* ctab, uint32_t* xsyn,
                                                uint64_t* zw, uint64_t bobmask, bool keep, uint32_t f, int tid,
                                                int wave, int lane) {
-    const uint32_t n_pad = (uint32_t)c.n_pad;
+    // (the code's sizes as scalars: through the DecodeArgs reference they are
+    // not known to be uniform)
+    const uint32_t n_pad = __builtin_amdgcn_readfirstlane((uint32_t)c.n_pad);
+    const int cn = __builtin_amdgcn_readfirstlane(c.n);
+    const int max_dv = __builtin_amdgcn_readfirstlane(c.max_dv);
     const float llr_p = (float)a.log_p;
     const float thr = (float)a.thr;
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
-    for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += kSp32Chunk) {
+    auto batch = [&](auto fullc, int r0) {
+        constexpr bool FULLC = decltype(fullc)::value;
         float v[kSp32Chunk][kDvUnroll];
         uint64_t bc[kSp32Chunk];
 #pragma unroll
         for (int u = 0; u < kSp32Chunk; ++u) {
             const int i = tid + (r0 + u) * kDecodeBlock;
-            const bool ok = i < c.n;
-            bc[u] = ok ? c.bit_code[i] : 0;
+            // (bit_code is padded to whole rounds, host.cpp build_code; rows
+            // k < max_dv of any i < n_pad are store slots: unconditional loads)
+            bc[u] = c.bit_code[i];
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k)     // (rows past max_dv have no slots)
-                v[u][k] = (FOLD || !ok || k >= c.max_dv) ? 0.0f : ms.ld((uint32_t)k * n_pad + i);
+                v[u][k] = (FOLD || (!DV3 && k >= max_dv)) ? 0.0f : ms.ld((uint32_t)k * n_pad + (uint32_t)i);
         }
 #pragma unroll
         for (int u = 0; u < kSp32Chunk; ++u) {
             const int r = r0 + u;
-            if (r * kDecodeBlock >= c.n) break;            // block-uniform
+            if (!FULLC && r * kDecodeBlock >= cn) break;            // block-uniform
             const int i = tid + r * kDecodeBlock;
-            const bool ok = i < c.n;
-            const int deg = (int)(bc[u] >> 48) & 3;
+            const bool ok = FULLC || i < cn;
+            const int deg = DV3 ? kDvUnroll : (int)(bc[u] >> 48) & 3;
             int32_t jc[kDvUnroll];
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k) jc[k] = (int32_t)(bc[u] >> (16 * k)) & 0xffff;
@@ -437,29 +545,41 @@ __device__ __forceinline__ void sp32_bit_phase(const DeviceCode& c, const Decode
                 }
             }
 #pragma unroll
-            for (int k = 0; k < kDvUnroll; ++k) acc = k < deg ? acc + v[u][k] : acc;
+            for (int k = 0; k < kDvUnroll; ++k) acc = (DV3 || k < deg) ? acc + v[u][k] : acc;
             const bool z = ok && acc <= 0.0f;
             const uint64_t zb = __ballot(z);
             const bool flip =
                 kRunSyn ? (ok && z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
-            if (lane == 0 && r * kDecodeBlock + wave * 64 < c.n) zw[(r * kDecodeBlock >> 6) + wave] = zb;
+            if (lane == 0 && (FULLC || r * kDecodeBlock + wave * 64 < cn)) zw[(r * kDecodeBlock >> 6) + wave] = zb;
             if (flip) {
 #pragma unroll
                 for (int k = 0; k < kDvUnroll; ++k)
-                    if (k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
+                    if (DV3 || k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
             }
-            if (!keep || !ok) continue;
+            if (!keep) continue;
+            // (lanes past N store into their own padding slots: no guard in
+            // full rounds; rows past a bit's degree are not stored)
 #pragma unroll
             for (int k = 0; k < kDvUnroll; ++k) {
-                if (k < deg) {
+                if (DV3 || (ok && k < deg)) {
                     float b = acc - v[u][k];
                     // keys path: b is finite (LLR +-log_p, clamped messages), where
                     // v_med3_f32 is clamp_msg exactly; LLR input may carry NaN
                     if (CLAMP) b = MODE == kModeKeys ? __builtin_amdgcn_fmed3f(b, -thr, thr) : clamp_msg(b, thr);
-                    ms.st((uint32_t)k * n_pad + i, b);
+                    if (DV3 && !FULLC) {
+                        if (ok) ms.st((uint32_t)k * n_pad + (uint32_t)i, b);
+                    } else {
+                        ms.st((uint32_t)k * n_pad + (uint32_t)i, b);
+                    }
                 }
             }
         }
+    };
+    using Full = std::integral_constant<bool, true>;
+    using Part = std::integral_constant<bool, false>;
+    for (int r0 = 0; __builtin_amdgcn_readfirstlane(r0 * kDecodeBlock) < cn; r0 += kSp32Chunk) {
+        if ((r0 + kSp32Chunk) * kDecodeBlock <= cn) batch(Full{}, r0);
+        else batch(Part{}, r0);
     }
 }
 
@@ -724,6 +844,7 @@ __device__ void fold_table_fill(const DeviceCode& c, const double* ctab, double 
 // rounds per load batch (2: measured -1 % per config-2 batch against 3, the
 // registers go to the check phases)
 constexpr int kIvChunk = QKD_IV_CHUNK;
+static_assert(kIvChunk - 1 <= kBitPadRounds, "per-bit arrays padded past the last load batch (host.cpp)");
 // DV3: every bit has exactly kDvUnroll (3) checks (a column-weight-3 code,
 // like the reference's N = 10240 one): no per-degree guards, so the round is
 // straight-line code except one branch around the hard decision's syndrome
@@ -1001,7 +1122,12 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     // QKD path: the first check phase folds into the first bit phase for both
     // sum-product rules (every b2c is +-log_p, so every message is +-C_d:
     // ctab); the second-iteration tanh table is the binary64 rule's only
-    constexpr bool FOLDS = MODE == kModeKeys && (RULE == kRuleSp64 || RULE == kRuleSp32);
+    // (min-sum: the self-corrected rule has no fold, its first check phase
+    // records every edge's b2c)
+    constexpr bool MSR = RULE == kRuleMinSumSplit || RULE == kRuleMinSumSplitSc;   // min-sum rules
+    constexpr bool MSC = RULE == kRuleMinSumSplitSc;
+    constexpr bool F32 = RULE != kRuleSp64;       // binary32 slots, all in LDS
+    constexpr bool FOLDS = MODE == kModeKeys && (RULE == kRuleSp64 || RULE == kRuleSp32 || RULE == kRuleMinSumSplit);
     constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
@@ -1017,11 +1143,13 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
     double* tab2 = reinterpret_cast<double*>(smem + L.tab2);
     float* wtab = reinterpret_cast<float*>(smem + L.wtab);
+    // (min-sum: the additive masks of ms_split_check_phase, 0 / +inf)
     for (int e = threadIdx.x; e < seg_weight_entries(DC); e += kDecodeBlock) {
         const int k = e % DC, p = (e / DC) % DC, deg = e / (DC * DC) + 1;
-        wtab[e] = (k < deg && k != p) ? 1.0f : 0.0f;
+        const bool in = k < deg && k != p;
+        wtab[e] = MSR ? (in ? 0.0f : __builtin_inff()) : (in ? 1.0f : 0.0f);
     }
-    using MS = SplitStore<T, RULE == kRuleSp32>;
+    using MS = SplitStore<T, F32>;
     T* const region = reinterpret_cast<T*>(a.c2b) + (size_t)region_of_block() * a.c2b_stride;
     const MS ms{
         reinterpret_cast<T*>(smem + L.msg),
@@ -1032,7 +1160,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     // the check phases' plan: encoded slot words for this layout (binary64
     // rule: DecodeArgs::plan_enc, built by the host from L), slot indices for
     // the all-LDS binary32 rule; the dummy column's slot in the same form
-    const uint2* const plan = RULE == kRuleSp64 ? a.plan_enc : c.plan_slot;
+    const uint2* const plan = (RULE == kRuleSp64 || MSR) ? a.plan_enc : c.plan_slot;
     const uint32_t dummy_w = encode_slot((uint32_t)c.n, L.S, (uint32_t)L.msg, (uint32_t)sizeof(T));
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1072,6 +1200,20 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             ctab[tid] = (double)v;
         }
     }
+    if constexpr (RULE == kRuleMinSumSplit && FOLDS) {
+        // the min-sum rule's first messages (every |b2c| = |float(log_p)|):
+        // scale * |log_p| - off, floored at 0, clamped, for every degree >= 2;
+        // degree 1 has no other edge (min over nothing: +inf)
+        if (tid <= kFirstTableDeg) {
+            float v = tid <= 1 ? __builtin_inff() : a.ms_scale * __builtin_fabsf((float)a.log_p);
+            if (a.ms_offset > 0.0f) v = __builtin_fmaxf(v - a.ms_offset, 0.0f);
+            if (CLAMP) v = clamp_msg(v, (float)a.thr);
+            ctab[tid] = (double)v;
+        }
+    }
+    // self-corrected min-sum: the previous b2c of each edge, two ballot words
+    // per task (ms_split_check_phase), in the ftab region (host: ftab_entries)
+    uint64_t* const scw = MSC ? reinterpret_cast<uint64_t*>(smem + L.ftab) : nullptr;
     if (tab2_on) {
         __syncthreads();
         second_table_fill<CLAMP>(c, ctab, a.log_p, a.thr, tab2, a.tab2_entries);
@@ -1288,7 +1430,14 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                     }
                 }
             } else if (!folded) {
-                if constexpr (RULE == kRuleSp32)
+                if constexpr (MSR) {
+                    if (a.ms_offset > 0.0f)
+                        ms_split_check_phase<CLAMP, DC, MSC, true>(plan, ms, row, wtab, scw, it > 0, n_tasks,
+                                                                   (float)thr, a.ms_scale, a.ms_offset, wave, lane);
+                    else
+                        ms_split_check_phase<CLAMP, DC, MSC, false>(plan, ms, row, wtab, scw, it > 0, n_tasks,
+                                                                    (float)thr, a.ms_scale, a.ms_offset, wave, lane);
+                } else if constexpr (RULE == kRuleSp32)
                     sp32_check_phase<CLAMP, DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, thr, wave, lane);
                 else if (TABLES && it == 1 && tab2_on)
                     split_check_phase<kSrcTable, CLAMP, DC, RULE>(plan, tsyn, tab2, ms, row, n_tasks, n_pad, thr,
@@ -1322,14 +1471,23 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                                                                f, tid, wave, lane);
                     }
                 }
-            } else if (RULE == kRuleSp32 && c.bit_code != nullptr) {
-                if constexpr (RULE == kRuleSp32) {
-                    if (folded)
-                        sp32_bit_phase<true, MODE, CLAMP>(c, a, ms, qsyn, ctab, xsyn, zw, bobmask, keep, f, tid, wave,
-                                                          lane);
-                    else
-                        sp32_bit_phase<false, MODE, CLAMP>(c, a, ms, qsyn, ctab, xsyn, zw, bobmask, keep, f, tid,
-                                                           wave, lane);
+            } else if (F32 && c.bit_code != nullptr) {
+                if constexpr (F32) {
+                    if (dv3) {
+                        if (folded)
+                            sp32_bit_phase<true, MODE, CLAMP, true>(c, a, ms, qsyn, ctab, xsyn, zw, bobmask, keep, f,
+                                                                    tid, wave, lane);
+                        else
+                            sp32_bit_phase<false, MODE, CLAMP, true>(c, a, ms, qsyn, ctab, xsyn, zw, bobmask, keep, f,
+                                                                     tid, wave, lane);
+                    } else {
+                        if (folded)
+                            sp32_bit_phase<true, MODE, CLAMP, false>(c, a, ms, qsyn, ctab, xsyn, zw, bobmask, keep, f,
+                                                                     tid, wave, lane);
+                        else
+                            sp32_bit_phase<false, MODE, CLAMP, false>(c, a, ms, qsyn, ctab, xsyn, zw, bobmask, keep,
+                                                                      f, tid, wave, lane);
+                    }
                 }
             } else
             for (int r0 = 0; r0 * kDecodeBlock < c.n; r0 += BC) {
@@ -1867,20 +2025,18 @@ __global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCo
     }
 }
 
-hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream) {
+hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream, bool gather, bool pack_first) {
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
     // the bit-sliced form when its slices fit LDS and the compact rows exist
-    // (QKD_SYN_SLICED=0: frame_syn_kernel; tests compare the two)
+    // (gather, the QKD_SYN_SLICED option 0: frame_syn_kernel; tests compare the two)
     const size_t slds = (size_t)a.words * 64 * sizeof(uint32_t);
-    const char* se = getenv("QKD_SYN_SLICED");
-    const bool sliced = a.code.chk_rows16 && slds <= 160 * 1024 && !(se && atoi(se) == 0);
+    const bool sliced = a.code.chk_rows16 && slds <= 160 * 1024 && !gather;
     // byte keys (qkd_qkd_ldpc_batch): packed by the sliced kernel itself when
-    // their rows allow 8-byte loads (QKD_SYN_BYTES=0: pack_kernel first; tests
-    // compare the two), else by pack_kernel
-    const char* sb = getenv("QKD_SYN_BYTES");
+    // their rows allow 8-byte loads (pack_first, the QKD_SYN_BYTES option 0: pack_kernel first;
+    // tests compare the two), else by pack_kernel
     const bool bytes = a.alice_b && sliced && a.code.n % 8 == 0 &&
                        ((reinterpret_cast<uintptr_t>(a.alice_b) | reinterpret_cast<uintptr_t>(a.bob_b)) & 7u) == 0 &&
-                       !(sb && atoi(sb) == 0);
+                       !pack_first;
     if (a.alice_b && !bytes) {
         const hipError_t e = launch_pack_keys(a, stream);
         if (e != hipSuccess) return e;
@@ -1943,8 +2099,24 @@ static DecodeFn pick_split_clamp(bool clamp, int max_dc, int* dc) {
     return clamp ? pick_split_dc<MODE, RULE, true>(max_dc, dc) : pick_split_dc<MODE, RULE, false>(max_dc, dc);
 }
 
+// the min-sum rules' buckets (the host takes them for check degree <= 8
+// only: the additive mask table)
+template <int MODE, int RULE, bool CLAMP>
+static DecodeFn pick_split_ms_dc(int max_dc, int* dc) {
+    if (max_dc <= 4) { *dc = 4; return decode_split_kernel<MODE, RULE, 4, CLAMP, 0>; }
+    if (max_dc <= 6) { *dc = 6; return decode_split_kernel<MODE, RULE, 6, CLAMP, 0>; }
+    *dc = 8;
+    return decode_split_kernel<MODE, RULE, 8, CLAMP, 0>;
+}
+template <int MODE, int RULE>
+static DecodeFn pick_split_ms(bool clamp, int max_dc, int* dc) {
+    return clamp ? pick_split_ms_dc<MODE, RULE, true>(max_dc, dc) : pick_split_ms_dc<MODE, RULE, false>(max_dc, dc);
+}
+
 template <int MODE>
 static DecodeFn pick_split_rule(int rule, bool clamp, int max_dc, int* dc) {
+    if (rule == kRuleMinSumSplit) return pick_split_ms<MODE, kRuleMinSumSplit>(clamp, max_dc, dc);
+    if (rule == kRuleMinSumSplitSc) return pick_split_ms<MODE, kRuleMinSumSplitSc>(clamp, max_dc, dc);
     if (rule == kRuleSp32) return pick_split_clamp<MODE, kRuleSp32>(clamp, max_dc, dc);
     return pick_split_clamp<MODE, kRuleSp64>(clamp, max_dc, dc);
 }

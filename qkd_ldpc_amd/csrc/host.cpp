@@ -31,6 +31,34 @@ qkd_status set_error(qkd_status s, const char* fmt, ...) {
 
 void clear_error() { g_last_error.clear(); }
 
+// ---- debug / A-B options (qkd_debug_set_option) -----------------------------
+static const char* const kDebugOptions[] = {
+    "QKD_SPEC_CAP", "QKD_SPEC_CKPT", "QKD_CKPT_UNSAT", "QKD_SPEC_POLICY", "QKD_FOLD_TABLE",
+    "QKD_DECODE_KERNEL", "QKD_MINSUM_STORE", "QKD_DECODE_GRID", "QKD_SPLIT_BUDGET", "QKD_C2B_PAD",
+    "QKD_ILV", "QKD_ILV_GRID", "QKD_KEYGEN", "QKD_SYN_SLICED", "QKD_SYN_BYTES", "QKD_BIT_ORDER",
+    "QKD_PHASE_TIMING"};
+static std::mutex g_dbg_mu;                            // guards g_dbg and every workspace's dbg
+static std::map<std::string, std::string> g_dbg;
+
+DbgOpt debug_option(const qkd_workspace* ws, const char* name) {
+    std::lock_guard<std::mutex> lock(g_dbg_mu);
+    DbgOpt o;
+    if (ws) {
+        const auto it = ws->dbg.find(name);
+        if (it != ws->dbg.end()) {
+            o.set = true;
+            o.v = it->second;
+            return o;
+        }
+    }
+    const auto it = g_dbg.find(name);
+    if (it != g_dbg.end()) {
+        o.set = true;
+        o.v = it->second;
+    }
+    return o;
+}
+
 static int32_t round_up(int32_t x, int32_t a) { return (x + a - 1) / a * a; }
 
 static void free_device(qkd_code* c) {
@@ -358,7 +386,8 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     std::vector<int32_t> perm(n), inv(n, -1);
     if (split) {
     // the split kernels' internal bit order (internal_bit_order)
-    internal_bit_order(n, c->n_pad, bdeg, plan, perm, inv, getenv("QKD_BIT_ORDER"));
+    const DbgOpt bit_order = debug_option(nullptr, "QKD_BIT_ORDER");
+    internal_bit_order(n, c->n_pad, bdeg, plan, perm, inv, bit_order ? bit_order.c_str() : nullptr);
     // the per-bit arrays in that order (the split kernels' DeviceCode view)
     std::vector<int32_t> bit_chk_s(bit_chk.size(), -1);
     std::vector<uint8_t> bit_deg_s(n, 0);
@@ -389,7 +418,9 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     QKD_HIP(hipMalloc(&c->d_bit_deg_s, bit_deg_s.size()));
     QKD_HIP(hipMemcpy(c->d_bit_deg_s, bit_deg_s.data(), bit_deg_s.size(), hipMemcpyHostToDevice));
     if (c->n_pat > 0) {
-        std::vector<uint16_t> bit_pat_s(std::max((size_t)n, (size_t)round_up(n, kDecodeBlock)), 0);
+        // (padded past the last whole load batch of the bit phases: they load
+        // every round of a batch unconditionally, decode_split.hip)
+        std::vector<uint16_t> bit_pat_s((size_t)round_up(n, kDecodeBlock) + kBitPadRounds * kDecodeBlock, 0);
         for (int32_t q = 0; q < n; ++q) bit_pat_s[q] = bit_pat[perm[q]];
         QKD_HIP(hipMalloc(&c->d_bit_pat_s, bit_pat_s.size() * sizeof(uint16_t)));
         QKD_HIP(hipMemcpy(c->d_bit_pat_s, bit_pat_s.data(), bit_pat_s.size() * sizeof(uint16_t),
@@ -399,9 +430,11 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
     // split kernels only: in the internal order
     bool packable = m <= 65536 && max_dv <= 3;
     for (int32_t j = 0; j < m && packable; ++j) packable = chk_deg[j] >= 1 && chk_deg[j] <= 16;
-    // (both padded with zeros to whole kDecodeBlock rounds: the speculative bit
-    // phase loads them unconditionally, decode_split.hip spec_bit_phase)
-    const size_t rounds_pad = std::max((size_t)c->n_pad, (size_t)round_up(n, kDecodeBlock));
+    // (both padded with zeros to whole kDecodeBlock rounds and kBitPadRounds
+    // more: the bit phases load whole batches of rounds unconditionally,
+    // decode_split.hip spec_bit_phase / sp32_bit_phase)
+    const size_t rounds_pad = std::max((size_t)c->n_pad, (size_t)round_up(n, kDecodeBlock)) +
+                              (size_t)kBitPadRounds * kDecodeBlock;
     if (packable) {
         std::vector<uint64_t> code(rounds_pad, 0);
         for (int32_t q = 0; q < n; ++q) {
@@ -694,6 +727,19 @@ qkd_code* qkd_code_from_dense(const char* path, int device, qkd_status* status) 
         return nullptr;
     }
     return make_code(n, m, cptr.data(), cidx.data(), device, status);
+}
+
+qkd_status qkd_debug_set_option(qkd_workspace* ws, const char* name, const char* value) {
+    clear_error();
+    if (!name) return set_error(QKD_ERR_INVALID_ARG, "option name is null");
+    bool known = false;
+    for (const char* k : kDebugOptions) known = known || !strcmp(k, name);
+    if (!known) return set_error(QKD_ERR_INVALID_ARG, "unknown debug option '%s'", name);
+    std::lock_guard<std::mutex> lock(g_dbg_mu);
+    std::map<std::string, std::string>& m = ws ? ws->dbg : g_dbg;
+    if (value) m[name] = value;
+    else m.erase(name);
+    return QKD_OK;
 }
 
 void qkd_code_destroy(qkd_code* code) {

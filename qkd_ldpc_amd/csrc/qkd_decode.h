@@ -55,7 +55,15 @@ enum DecodeMode : int {
 //   kRuleMinSumLdsSc  kRuleMinSumLds with Savin's self-correction
 //               (QKD_MINSUM_SELF_CORRECT) compiled in: its own kernel
 //               instantiation, so profiles attribute its time to it
-enum DecodeRule : int { kRuleSp64 = 0, kRuleSp32 = 1, kRuleMinSum = 2, kRuleMinSumLds = 3, kRuleMinSumLdsSc = 4 };
+//   kRuleMinSumSplit / kRuleMinSumSplitSc  the same min-sum rules (plain /
+//               self-corrected) on the split decoder's skeleton: one binary32
+//               slot per edge, all in LDS, edge-parallel check phase
+//               (decode_split.hip ms_split_check_phase); used whenever that
+//               store fits (the default for codes like the reference's)
+enum DecodeRule : int {
+    kRuleSp64 = 0, kRuleSp32 = 1, kRuleMinSum = 2, kRuleMinSumLds = 3, kRuleMinSumLdsSc = 4,
+    kRuleMinSumSplit = 5, kRuleMinSumSplitSc = 6
+};
 template <int RULE> struct RuleMsg { using T = float; };
 template <> struct RuleMsg<kRuleSp64> { using T = double; };
 
@@ -642,7 +650,9 @@ DecodeFn pick_split_spec(int mode, int max_dc, bool ckpt, int* dc);
 DecodeFn pick_ilv(int rs, int max_dc, bool tsyn_global);
 // decode_split.hip, kModeKeys: the kernels around the split decoder.
 // Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.
-hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream);
+// gather: the gather kernel instead of the bit-sliced one; pack_first: byte
+// keys packed by pack_kernel first (the QKD_SYN_SLICED / QKD_SYN_BYTES options)
+hipError_t launch_frame_syn(const DecodeArgs& a, hipStream_t stream, bool gather = false, bool pack_first = false);
 // decode.hip: a.alice_b / a.bob_b -> a.alice_w / a.bob_w (original bit order)
 hipError_t launch_pack_keys(const DecodeArgs& a, hipStream_t stream);
 hipError_t launch_key_match(const DecodeArgs& a, hipStream_t stream);

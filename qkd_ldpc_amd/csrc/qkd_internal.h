@@ -4,6 +4,7 @@
 
 #include <cstdarg>
 #include <cstdint>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
@@ -25,6 +26,9 @@ constexpr int kTab2MaxDv = 3;   // <= the bit phase's unrolled rows (decode.hip 
 constexpr int kTab2MaxEntries = 2048;
 constexpr int kFoldTabMaxEntries = 1024;   // speculative fold table (decode_split.hip), 8 B each
 constexpr size_t kC2bPad = 64;             // split kernels: slots added to each workgroup's global region
+// per-bit arrays of the split kernels (bit_code, bit_pat): rounds of padding
+// past the last round, >= the largest bit-phase load batch minus one
+constexpr int kBitPadRounds = 4;
 __host__ __device__ inline int tab2_stride(int max_dv) { return (1 << (1 + max_dv)) * max_dv; }
 
 // Largest check degree: one check's edges fit one wavefront (qkd_plan.h).
@@ -139,6 +143,8 @@ struct qkd_workspace {
     const qkd_code* code = nullptr;
     int device = 0;
     std::mutex mu;
+    // qkd_debug_set_option values of this workspace (host.cpp debug_option)
+    std::map<std::string, std::string> dbg;
     // decode scratch: one c2b region per resident workgroup
     double* c2b = nullptr;
     size_t c2b_slots = 0;
@@ -266,6 +272,20 @@ namespace qkd {
 
 qkd_status set_error(qkd_status s, const char* fmt, ...);
 void clear_error();
+
+// A debug / A-B option (qkd_debug_set_option, host.cpp): the workspace's
+// value, else the process-wide one, else unset (the product behaviour). The
+// library reads no environment variable.
+struct DbgOpt {
+    bool set = false;
+    std::string v;
+    explicit operator bool() const { return set; }
+    const char* c_str() const { return v.c_str(); }
+    int as_int() const { return atoi(v.c_str()); }
+    long as_long() const { return atol(v.c_str()); }
+    bool is(const char* s) const { return set && v == s; }
+};
+DbgOpt debug_option(const qkd_workspace* ws, const char* name);
 
 struct DeviceGuard {
     int prev = -1;

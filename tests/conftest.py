@@ -50,6 +50,24 @@ def oracle_code(golden_code, oracle_mod):
     return oracle_mod.Code.from_lists(golden_code)
 
 
+@pytest.fixture
+def qkd_opt():
+    """Sets process-wide debug options of the library (qkd_debug_set_option;
+    the library reads no environment variable) for one test:
+    qkd_opt("QKD_SPEC_CAP", 0); qkd_opt(name, None) restores the default.
+    Every option it touched is restored at teardown."""
+    import qkd_ldpc_amd as Q
+    touched = set()
+
+    def set_opt(name, value=None):
+        touched.add(name)
+        Q.set_debug_option(name, value)
+
+    yield set_opt
+    for name in touched:
+        Q.set_debug_option(name, None)
+
+
 def write_alist(path, n, m, bit_off, bit_idx, chk_off, chk_idx, pad=True):
     """Emit an alist file (1-based, zero-padded rows) from adjacency arrays."""
     dv = np.diff(bit_off)

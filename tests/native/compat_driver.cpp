@@ -13,6 +13,7 @@
 //   syndrome                     then a line of n bits
 //   trial <q> <seed>
 //   batch <npoints> <q>...       QKD_LDPC_batch_simulation over one matrix
+//   variant <name>               qkd_amd_set_variant (the shim's decoder variant)
 #include <cstdio>
 #include <iostream>
 #include <sstream>
@@ -98,6 +99,11 @@ int main() {
                 fresh.check_nodes = keep;
                 H = fresh;
                 std::printf("ok recode %d\n", (int)H.is_regular);
+            } else if (cmd == "variant") {
+                std::string name;
+                std::cin >> name;
+                qkd_amd_set_variant(name.c_str());
+                std::printf("ok variant\n");
             } else if (cmd == "cfg") {
                 int on;
                 std::cin >> CFG.SUM_PRODUCT_MAX_ITERATIONS >> CFG.SUM_PRODUCT_MSG_LLR_THRESHOLD >> on >>

@@ -191,6 +191,34 @@ def test_dense_reader_errors(N, tmp_path):
     assert st == N.ERR_IO and "Column" in msg or "Row" in msg
 
 
+def test_library_reads_no_environment():
+    """Product behaviour never depends on the process environment: neither the
+    HIP library nor the compatibility shim imports getenv (debug and A/B
+    options go through qkd_debug_set_option / qkd_amd_set_*)."""
+    libs = [os.path.join(ROOT, "qkd_ldpc_amd", "lib", "libqkd_ldpc_amd.so")]
+    shim = os.path.join(ROOT, "qkd_ldpc_amd", "lib", "libqkd_ldpc_compat.so")
+    if os.path.exists(shim):
+        libs.append(shim)
+    for lib in libs:
+        out = subprocess.check_output(["nm", "-D", "--undefined-only", lib], text=True)
+        names = {ln.split()[-1].split("@")[0] for ln in out.splitlines() if ln.strip()}
+        assert not names & {"getenv", "secure_getenv", "__libc_secure_getenv"}, lib
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "qkd_ldpc_amd", "csrc")):
+        for f in files:
+            assert "getenv" not in open(os.path.join(dirpath, f), errors="replace").read(), f
+
+
+def test_debug_options_validated(N):
+    """qkd_debug_set_option: known names set and reset (process-wide, no device
+    needed), unknown names are errors."""
+    L = N.lib()
+    assert L.qkd_debug_set_option(None, b"QKD_SPEC_CAP", b"3") == 0
+    assert L.qkd_debug_set_option(None, b"QKD_SPEC_CAP", None) == 0
+    assert L.qkd_debug_set_option(None, b"QKD_NO_SUCH_OPTION", b"1") != 0
+    assert "unknown debug option" in N.last_error()
+    assert L.qkd_debug_set_option(None, None, b"1") != 0
+
+
 def test_product_never_imports_oracle():
     """The oracle is test infrastructure: no product source references it."""
     for dirpath, _, files in os.walk(os.path.join(ROOT, "qkd_ldpc_amd")):

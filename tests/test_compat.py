@@ -200,17 +200,17 @@ def test_compat_too_small_qber_throws_reference_message(driver):
 
 
 @pytest.mark.gpu
-def test_compat_variant_env_selects_minsum(driver, golden_code, oracle_mod):
-    """QKD_AMD_VARIANT=minsum runs the reference harness on the min-sum variant:
-    its batch point equals the library's own min-sum trials; an unknown name
-    throws like the reference's errors do."""
+def test_compat_variant_selects_minsum(driver, golden_code, oracle_mod):
+    """qkd_amd_set_variant("minsum") runs the reference harness on the min-sum
+    variant: its batch point equals the library's own min-sum trials; an
+    unknown name throws like the reference's errors do. (The shim reads no
+    environment variable.)"""
     import qkd_ldpc_amd as Q
     import torch
     g = golden_code
-    lines = _code_cmd(10240, 5231, g["chk_off"], g["chk_idx"]) + ["cfg 50 100.0 1 512 777", "batch 1 0.06"]
-    env = dict(os.environ, QKD_AMD_VARIANT="minsum")
-    p = subprocess.run([driver], input="\n".join(lines) + "\n", text=True, capture_output=True,
-                       timeout=600, env=env)
+    lines = _code_cmd(10240, 5231, g["chk_off"], g["chk_idx"]) + ["variant minsum", "cfg 50 100.0 1 512 777",
+                                                                   "batch 1 0.06"]
+    p = subprocess.run([driver], input="\n".join(lines) + "\n", text=True, capture_output=True, timeout=600)
     assert p.returncode == 0, p.stderr
     v = [ln for ln in p.stdout.splitlines() if ln.startswith("point")][0].split()
     H = Q.HMatrix.from_check_lists(10240, g["chk_off"], g["chk_idx"])
@@ -222,7 +222,6 @@ def test_compat_variant_env_selects_minsum(driver, golden_code, oracle_mod):
     st = oracle_mod.batch_stats(it, sp, r.keys_match.cpu().numpy(), r.exact_qber.cpu().numpy(), 512, 50)
     assert float(v[3]) == st["iterations_successful_sp_mean"]
     assert float(v[8]) == st["ratio_trials_successful_ldpc"]
-    env["QKD_AMD_VARIANT"] = "bogus"
-    p = subprocess.run([driver], input="\n".join(lines) + "\n", text=True, capture_output=True,
-                       timeout=600, env=env)
+    lines[lines.index("variant minsum")] = "variant bogus"
+    p = subprocess.run([driver], input="\n".join(lines) + "\n", text=True, capture_output=True, timeout=600)
     assert "unknown decoder variant 'bogus'" in p.stdout + p.stderr

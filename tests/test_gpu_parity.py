@@ -197,10 +197,10 @@ def test_decoded_qber_of_one_rejected(Q, H):
 # ---- fused trials: BASELINE configs 2 and 3 per frame ----------------------------------
 
 @pytest.mark.parametrize("sliced", ["1", "0"])
-def test_trials_config2_full_batch(Q, H, probe, golden_vectors, monkeypatch, sliced):
+def test_trials_config2_full_batch(Q, H, probe, golden_vectors, monkeypatch, sliced, qkd_opt):
     """sliced 1: the frame syndromes and internal-order keys by
     frame_syn_sliced_kernel (the default); 0: by frame_syn_kernel."""
-    monkeypatch.setenv("QKD_SYN_SLICED", sliced)
+    qkd_opt("QKD_SYN_SLICED", sliced)
     seeds = Q.make_seeds(777, 4096)
     r = Q.run_trials(H, seeds_dev(seeds), 0.02, 0, 50, 100.0, True)
     torch.cuda.synchronize()
@@ -248,13 +248,13 @@ def test_qkd_ldpc_batch_matches_trials(Q, H, golden_vectors):
 
 
 @pytest.mark.parametrize("form", ["bytes", "pack", "bytes_misaligned"])
-def test_qkd_ldpc_byte_keys_forms(Q, H, golden_vectors, monkeypatch, form):
+def test_qkd_ldpc_byte_keys_forms(Q, H, golden_vectors, monkeypatch, form, qkd_opt):
     """qkd_qkd_ldpc_batch's byte keys: packed inside frame_syn_sliced_kernel (the
     default when rows allow 8-byte loads), by pack_kernel first (QKD_SYN_BYTES=0),
     and from 4- but not 8-byte-aligned arrays (pack_kernel, chosen by the launcher);
     1000 frames (the last 16-frame group ragged). Decoded words, iterations and flags
     equal the golden config-2 frames."""
-    monkeypatch.setenv("QKD_SYN_BYTES", "0" if form == "pack" else "1")
+    qkd_opt("QKD_SYN_BYTES", "0" if form == "pack" else "1")
     F = 1000
     seeds = seeds_dev(Q.make_seeds(777, F))
     a, b, q = Q.keygen(H, seeds, 0.02)
@@ -376,13 +376,13 @@ def test_device_math_bit_exact_vs_glibc(Q, oracle_mod, which):
 
 
 @pytest.mark.parametrize("mode", ["fast", "lanes", "matrix", "replay", "serial"])
-def test_keygen_kernels_agree_with_oracle(Q, oracle_mod, monkeypatch, mode):
+def test_keygen_kernels_agree_with_oracle(Q, oracle_mod, monkeypatch, mode, qkd_opt):
     """The two-wave jump-ahead generator (default), its serial regeneration
     (taken after a Lemire rejection; forced here), the one-wave generator with
     polynomial and matrix jumps, and the one-thread-per-frame kernel all
     reproduce run_trial's keys."""
     if mode != "fast":
-        monkeypatch.setenv("QKD_KEYGEN", mode)
+        qkd_opt("QKD_KEYGEN", mode)
     rng = np.random.default_rng(31)
     for n, q in [(2, 0.5), (3, 1.0), (6, 0.5), (10, 1.0), (64, 0.1), (65, 0.5), (127, 0.3),
                  (1001, 0.02), (4100, 1.0), (10240, 0.3), (10240, 0.45)]:
@@ -458,12 +458,12 @@ def _chain_code(Q, n):
 
 
 @pytest.mark.parametrize("mode", ["fast", "replay"])
-def test_keygen_beyond_65536_bits(Q, oracle_mod, monkeypatch, mode):
+def test_keygen_beyond_65536_bits(Q, oracle_mod, monkeypatch, mode, qkd_opt):
     """The two-wave generator at and past N = 65536, where its Lemire products leave
     32 bits (keygen_split_kernel<false>: binary64 quotients, 64-bit draw indices),
     and its serial regeneration path there: keys and exact QBER equal run_trial's."""
     if mode != "fast":
-        monkeypatch.setenv("QKD_KEYGEN", mode)
+        qkd_opt("QKD_KEYGEN", mode)
     rng = np.random.default_rng(65)
     for n, q in [(65536, 0.02), (65536, 0.05), (65537, 0.02), (70001, 0.03)]:
         H = _chain_code(Q, n)

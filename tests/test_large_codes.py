@@ -85,9 +85,9 @@ def big_codes(big, Q, oracle_mod, tmp_path_factory):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel", ["split", "classic"])
 @pytest.mark.parametrize("q,thr,thr_on", [(0.03, 100.0, True), (0.06, 2.5, True), (0.04, 0.0, False)])
-def test_large_code_decode_bit_exact(Q, big_codes, oracle_mod, monkeypatch, kernel, q, thr, thr_on):
+def test_large_code_decode_bit_exact(Q, big_codes, oracle_mod, monkeypatch, kernel, q, thr, thr_on, qkd_opt):
     if kernel == "classic":
-        monkeypatch.setenv("QKD_DECODE_KERNEL", "classic")
+        qkd_opt("QKD_DECODE_KERNEL", "classic")
     H, oc = big_codes
     n = H.num_bit_nodes
     frames = []
@@ -110,11 +110,11 @@ def test_large_code_decode_bit_exact(Q, big_codes, oracle_mod, monkeypatch, kern
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel", ["split", "classic"])
 @pytest.mark.parametrize("q", [0.03, 0.05, 0.11])
-def test_large_code_trials_equal_oracle(Q, big_codes, oracle_mod, monkeypatch, kernel, q):
+def test_large_code_trials_equal_oracle(Q, big_codes, oracle_mod, monkeypatch, kernel, q, qkd_opt):
     """Fused trials (keygen + decode + compare); at q = 0.11 floor(N q) = 4400
     flips take the serial key generator."""
     if kernel == "classic":
-        monkeypatch.setenv("QKD_DECODE_KERNEL", "classic")
+        qkd_opt("QKD_DECODE_KERNEL", "classic")
     H, oc = big_codes
     seeds = oracle_mod.seeds(777, 8)
     r = Q.run_trials(H, torch.from_numpy(seeds.view(np.int64)).cuda(), q, 0, 40)
@@ -138,7 +138,7 @@ def test_large_code_variants_decode(Q, big_codes, variant):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dv,dc,n", [(3, 6, 2400), (3, 12, 2400), (2, 16, 2400), (3, 6, 2460)])
-def test_frame_syn_sliced_equals_plain(monkeypatch, dv, dc, n):
+def test_frame_syn_sliced_equals_plain(monkeypatch, dv, dc, n, qkd_opt):
     """frame_syn_sliced_kernel (frames bit-sliced, uint16 check rows of width
     8 or 16) against frame_syn_kernel (QKD_SYN_SLICED=0): the
     same decoded words, iterations and flags on the keys path."""
@@ -151,7 +151,7 @@ def test_frame_syn_sliced_equals_plain(monkeypatch, dv, dc, n):
     a, b, q = Q.keygen(H, seeds, 0.01)
     out = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("QKD_SYN_SLICED", mode)
+        qkd_opt("QKD_SYN_SLICED", mode)
         r = Q.qkd_ldpc(H, a, b, float(q[0]), 50, 100.0, True, want_bits=True)
         torch.cuda.synchronize()
         out[mode] = r
@@ -162,13 +162,13 @@ def test_frame_syn_sliced_equals_plain(monkeypatch, dv, dc, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("q,grid", [(0.03, 1), (0.05, 2), (0.08, 3)])
-def test_interleaved_trials_equal_oracle(Q, big_codes, oracle_mod, monkeypatch, q, grid):
+def test_interleaved_trials_equal_oracle(Q, big_codes, oracle_mod, monkeypatch, q, grid, qkd_opt):
     """The frame-interleaved decoder (decode_ilv.hip, forced with QKD_ILV=1)
     against the oracle: 40 frames through 1-3 workgroups, so columns take
     several frames each (the queue refill); at q = 0.08 frames hand off to the
     split kernel's exact replays."""
-    monkeypatch.setenv("QKD_ILV", "1")
-    monkeypatch.setenv("QKD_ILV_GRID", str(grid))
+    qkd_opt("QKD_ILV", "1")
+    qkd_opt("QKD_ILV_GRID", str(grid))
     H, oc = big_codes
     seeds = oracle_mod.seeds(123, 40)
     r = Q.run_trials(H, torch.from_numpy(seeds.view(np.int64)).cuda(), q, 0, 40)
@@ -182,7 +182,7 @@ def test_interleaved_trials_equal_oracle(Q, big_codes, oracle_mod, monkeypatch, 
 @pytest.mark.gpu
 @pytest.mark.parametrize("q,cap,frames", [(0.02, None, 4096), (0.03, None, 4096), (0.03, "2", 4096),
                                           (0.05, None, 4096), (0.04, None, 10000)])
-def test_interleaved_equals_split_at_scale(Q, big_codes, monkeypatch, q, cap, frames):
+def test_interleaved_equals_split_at_scale(Q, big_codes, monkeypatch, q, cap, frames, qkd_opt):
     """4096 frames: the interleaved decoder (its default for this code at this
     batch size) and the split kernel (QKD_ILV=0) give the same iterations,
     syndrome and key flags. QKD_SPEC_CAP=2 hands every frame still iterating
@@ -190,12 +190,12 @@ def test_interleaved_equals_split_at_scale(Q, big_codes, monkeypatch, q, cap, fr
     10,000 frames take the columns through two to three frames each."""
     H, _ = big_codes
     if cap:
-        monkeypatch.setenv("QKD_SPEC_CAP", cap)
+        qkd_opt("QKD_SPEC_CAP", cap)
     seeds = torch.from_numpy(Q.make_seeds(2024, frames).view(np.int64)).cuda()
     a, b, qq = Q.keygen(H, seeds, q)
     out = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("QKD_ILV", mode)
+        qkd_opt("QKD_ILV", mode)
         r = Q.qkd_ldpc(H, a, b, float(qq[0]), 50)
         torch.cuda.synchronize()
         out[mode] = r
@@ -206,7 +206,7 @@ def test_interleaved_equals_split_at_scale(Q, big_codes, monkeypatch, q, cap, fr
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("q", [0.02, 0.04])
-def test_interleaved_global_targets_equal_split(Q, monkeypatch, q):
+def test_interleaved_global_targets_equal_split(Q, monkeypatch, q, qkd_opt):
     """N = 60,000 (M = 30,000): the interleaved decoder's three LDS syndrome
     arrays would not fit, so its target syndrome words live in global memory
     (decode_ilv_kernel<..., TG = true>); 1024 frames give the same iterations,
@@ -218,7 +218,7 @@ def test_interleaved_global_targets_equal_split(Q, monkeypatch, q):
     a, b, qq = Q.keygen(H, seeds, q)
     out = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("QKD_ILV", mode)
+        qkd_opt("QKD_ILV", mode)
         r = Q.qkd_ldpc(H, a, b, float(qq[0]), 50)
         torch.cuda.synchronize()
         out[mode] = r

@@ -190,8 +190,8 @@ def test_phi_bounds_out_at_zero(Q):
 
 
 @pytest.mark.parametrize("cap", ["0", "1", "2", "3", "8", "50"])
-def test_trials_config2_every_cap(Q, H, golden_vectors, monkeypatch, cap):
-    monkeypatch.setenv("QKD_SPEC_CAP", cap)
+def test_trials_config2_every_cap(Q, H, golden_vectors, monkeypatch, cap, qkd_opt):
+    qkd_opt("QKD_SPEC_CAP", cap)
     seeds = seeds_dev(Q.make_seeds(777, 4096))
     ws = Q.Workspace(H)
     replays(Q, ws)
@@ -207,8 +207,8 @@ def test_trials_config2_every_cap(Q, H, golden_vectors, monkeypatch, cap):
 
 
 @pytest.mark.parametrize("cap", ["2", "8", "50"])
-def test_trials_config3_points_every_cap(Q, H, golden_vectors, monkeypatch, cap):
-    monkeypatch.setenv("QKD_SPEC_CAP", cap)
+def test_trials_config3_points_every_cap(Q, H, golden_vectors, monkeypatch, cap, qkd_opt):
+    qkd_opt("QKD_SPEC_CAP", cap)
     seeds = seeds_dev(Q.make_seeds(777, 10000))
     ws = Q.Workspace(H)
     grid = golden_vectors["c3_qnom"]
@@ -224,10 +224,10 @@ def test_trials_config3_points_every_cap(Q, H, golden_vectors, monkeypatch, cap)
 
 @pytest.mark.parametrize("q,max_it", [(0.05, 50), (0.09, 50), (0.11, 12), (0.15, 6)])
 @pytest.mark.parametrize("thr", [100.0, 2.5, 0.7])
-def test_spec_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, thr):
+def test_spec_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, thr, qkd_opt):
     """Decoded words of converging and failing frames (the cap at max_it lets the
     speculative iterations run to the end) equal the oracle's bit for bit."""
-    monkeypatch.setenv("QKD_SPEC_CAP", "64")
+    qkd_opt("QKD_SPEC_CAP", "64")
     rng = np.random.default_rng(int(q * 1000) + int(thr * 10))
     f = 4
     alice = rng.integers(0, 2, (f, 10240))
@@ -248,12 +248,12 @@ def test_spec_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, thr):
 
 @pytest.mark.parametrize("cap", ["0", "8"])
 @pytest.mark.parametrize("q", [0.02, 0.05])
-def test_spec_llr_path_matches_oracle(Q, H, oracle_code, monkeypatch, cap, q):
+def test_spec_llr_path_matches_oracle(Q, H, oracle_code, monkeypatch, cap, q, qkd_opt):
     """qkd_decode_batch (the reference's sum_product_decoding, LLR input) with
     the speculation on and off: decoded words, iteration counts and flags equal
     the oracle's; the LLR path has no folded first iteration, so the intervals
     start from the LLRs themselves."""
-    monkeypatch.setenv("QKD_SPEC_CAP", cap)
+    qkd_opt("QKD_SPEC_CAP", cap)
     rng = np.random.default_rng(int(q * 1000))
     f = 24
     alice = rng.integers(0, 2, (f, 10240))
@@ -277,14 +277,14 @@ def test_spec_llr_path_matches_oracle(Q, H, oracle_code, monkeypatch, cap, q):
     print(f"LLR path cap {cap} q {q}: {Q.spec_replays(ws)} of {f} replayed")
 
 
-def test_spec_policy_turns_off_at_high_qber(Q, H, golden_vectors, monkeypatch):
+def test_spec_policy_turns_off_at_high_qber(Q, H, golden_vectors, monkeypatch, qkd_opt):
     """At QBER 0.08 most frames cannot be certified: the first call replays
     many (the in-launch policy stops speculating after a sixth), later calls on
     the workspace skip the speculation for that QBER and up (QKD_CKPT_UNSAT=0:
     no checkpointed speculation either); the results are the golden ones
     throughout."""
-    monkeypatch.setenv("QKD_SPEC_CAP", "8")
-    monkeypatch.setenv("QKD_CKPT_UNSAT", "0")
+    qkd_opt("QKD_SPEC_CAP", "8")
+    qkd_opt("QKD_CKPT_UNSAT", "0")
     seeds = seeds_dev(Q.make_seeds(777, 10000))
     grid = golden_vectors["c3_qnom"]
     s = int(np.argmin(np.abs(grid - 0.08)))
@@ -302,14 +302,14 @@ def test_spec_policy_turns_off_at_high_qber(Q, H, golden_vectors, monkeypatch):
 
 
 @pytest.mark.parametrize("trigger", ["16", "128", "1024"])
-def test_ckpt_config3_points(Q, H, golden_vectors, monkeypatch, trigger):
+def test_ckpt_config3_points(Q, H, golden_vectors, monkeypatch, trigger, qkd_opt):
     """Checkpointed speculation (SPEC 2) forced at every config-3 point: exact
     iterations until fewer than `trigger` checks are unsatisfied, intervals
     from a saved message store, restores on failure (a trigger of 1024 makes
     most attempts fail and exercises the restores); golden results."""
-    monkeypatch.setenv("QKD_SPEC_CAP", "8")
-    monkeypatch.setenv("QKD_SPEC_CKPT", "1")
-    monkeypatch.setenv("QKD_CKPT_UNSAT", trigger)
+    qkd_opt("QKD_SPEC_CAP", "8")
+    qkd_opt("QKD_SPEC_CKPT", "1")
+    qkd_opt("QKD_CKPT_UNSAT", trigger)
     seeds = seeds_dev(Q.make_seeds(777, 10000))
     ws = Q.Workspace(H)
     grid = golden_vectors["c3_qnom"]
@@ -329,13 +329,13 @@ def test_ckpt_config3_points(Q, H, golden_vectors, monkeypatch, trigger):
 
 
 @pytest.mark.parametrize("q,max_it,cap", [(0.07, 50, "8"), (0.09, 50, "64"), (0.11, 20, "64"), (0.08, 12, "3")])
-def test_ckpt_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, cap):
+def test_ckpt_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, cap, qkd_opt):
     """Decoded words after checkpointed speculation (converging frames, frames
     that fail with the intervals running to max_it, caps that force restores)
     equal the oracle's bit for bit."""
-    monkeypatch.setenv("QKD_SPEC_CAP", cap)
-    monkeypatch.setenv("QKD_SPEC_CKPT", "1")
-    monkeypatch.setenv("QKD_CKPT_UNSAT", "400")
+    qkd_opt("QKD_SPEC_CAP", cap)
+    qkd_opt("QKD_SPEC_CKPT", "1")
+    qkd_opt("QKD_CKPT_UNSAT", "400")
     rng = np.random.default_rng(int(q * 1000) + max_it)
     f = 6
     alice = rng.integers(0, 2, (f, 10240))
@@ -352,13 +352,13 @@ def test_ckpt_bits_match_oracle(Q, H, oracle_code, monkeypatch, q, max_it, cap):
         assert (bits[k] == want["out"]).all(), (q, k)
 
 
-def test_ckpt_policy_default(Q, H, golden_vectors, monkeypatch):
+def test_ckpt_policy_default(Q, H, golden_vectors, monkeypatch, qkd_opt):
     """Default policy at QBER 0.07: the first call speculates from the first
     iteration and replays too many frames; the next calls switch to the
     checkpointed speculation; golden results throughout."""
-    monkeypatch.delenv("QKD_SPEC_CAP", raising=False)
-    monkeypatch.delenv("QKD_CKPT_UNSAT", raising=False)
-    monkeypatch.delenv("QKD_SPEC_CKPT", raising=False)
+    qkd_opt("QKD_SPEC_CAP", None)
+    qkd_opt("QKD_CKPT_UNSAT", None)
+    qkd_opt("QKD_SPEC_CKPT", None)
     seeds = seeds_dev(Q.make_seeds(777, 10000))
     grid = golden_vectors["c3_qnom"]
     s = int(np.argmin(np.abs(grid - 0.07)))
@@ -409,16 +409,16 @@ def fresh_seeds(Q):
 
 
 @pytest.mark.parametrize("q", [0.02, 0.03, 0.04, 0.05, 0.06, 0.07, 0.08])
-def test_spec_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q):
+def test_spec_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q, qkd_opt):
     """100,000 frames per QBER point that no golden vector covers: the default
     (speculative, policy-driven, run twice so the per-workspace policy settles and
     both of its modes run) against the exact iterations alone (QKD_SPEC_CAP=0):
     decoded words, iteration counts and flags identical."""
     ws = Q.Workspace(H)
     alice, bob, _ = Q.keygen(H, fresh_seeds, q, 0, workspace=ws)
-    monkeypatch.setenv("QKD_SPEC_CAP", "0")
+    qkd_opt("QKD_SPEC_CAP", "0")
     ex = Q.qkd_ldpc(H, alice, bob, q, 50, 100.0, True, want_bits=True, workspace=ws)
-    monkeypatch.delenv("QKD_SPEC_CAP")
+    qkd_opt("QKD_SPEC_CAP", None)
     ws2 = Q.Workspace(H)
     Q.spec_replays(ws2, reset=True)
     for rep in range(2):
@@ -434,7 +434,7 @@ def test_spec_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q):
 
 
 @pytest.mark.parametrize("q", [0.02, 0.04, 0.06])
-def test_fold_table_equals_per_bit_form(Q, H, fresh_seeds, monkeypatch, q):
+def test_fold_table_equals_per_bit_form(Q, H, fresh_seeds, monkeypatch, q, qkd_opt):
     """The speculative kernel's folded first iteration from its per-pattern table
     (fold_table_fill) against the per-bit form (QKD_FOLD_TABLE=0): the same psi
     bounds give the same certified rounds, so outputs AND the count of frames the
@@ -444,7 +444,7 @@ def test_fold_table_equals_per_bit_form(Q, H, fresh_seeds, monkeypatch, q):
     seeds = fresh_seeds[:20_000]
     out = {}
     for tab in ("0", "1"):
-        monkeypatch.setenv("QKD_FOLD_TABLE", tab)
+        qkd_opt("QKD_FOLD_TABLE", tab)
         ws = Q.Workspace(H)
         alice, bob, _ = Q.keygen(H, seeds, q, 0, workspace=ws)
         Q.spec_replays(ws, reset=True)
@@ -458,7 +458,7 @@ def test_fold_table_equals_per_bit_form(Q, H, fresh_seeds, monkeypatch, q):
 
 
 @pytest.mark.parametrize("q", [0.02, 0.05])
-def test_spec_llr_path_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q):
+def test_spec_llr_path_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypatch, q, qkd_opt):
     """The LLR entry (sum_product_decoding) on 100,000 fresh frames with LLRs that are
     not +-log_p (each scaled by 1 + U(0, 0.25)): speculative = exact."""
     ws = Q.Workspace(H)
@@ -469,9 +469,9 @@ def test_spec_llr_path_matches_exact_on_fresh_frames(Q, H, fresh_seeds, monkeypa
     scale = 1.0 + 0.25 * torch.rand(bob.shape, dtype=torch.float64, device="cuda", generator=g)
     llr = torch.where(bob == 1, -lp, lp) * scale
     syn = Q.calculate_syndrome(H, alice)
-    monkeypatch.setenv("QKD_SPEC_CAP", "0")
+    qkd_opt("QKD_SPEC_CAP", "0")
     ex = Q.sum_product_decoding(H, llr, syn, 50, 100.0, True, workspace=ws)
-    monkeypatch.delenv("QKD_SPEC_CAP")
+    qkd_opt("QKD_SPEC_CAP", None)
     sp = Q.sum_product_decoding(H, llr, syn, 50, 100.0, True, workspace=Q.Workspace(H))
     torch.cuda.synchronize()
     assert torch.equal(sp.iterations, ex.iterations)
@@ -502,7 +502,7 @@ def test_psi_of_exact_pair_equals_scalar(Q):
 
 
 @pytest.mark.parametrize("q", [0.05, 0.08])
-def test_replay_policy_independent_of_scheduling(Q, H, fresh_seeds, monkeypatch, q):
+def test_replay_policy_independent_of_scheduling(Q, H, fresh_seeds, monkeypatch, q, qkd_opt):
     """The in-launch replay policy (decode_split.hip spec_policy) decides frame f from
     window f / 256 - 8 of the frame index, so the frames it keeps off the speculation,
     and with them the replay count, are the same whatever order the workgroups finish
@@ -513,9 +513,9 @@ def test_replay_policy_independent_of_scheduling(Q, H, fresh_seeds, monkeypatch,
     out = {}
     for grid in ("0", "97", "160"):
         if grid == "0":
-            monkeypatch.delenv("QKD_DECODE_GRID", raising=False)
+            qkd_opt("QKD_DECODE_GRID", None)
         else:
-            monkeypatch.setenv("QKD_DECODE_GRID", grid)
+            qkd_opt("QKD_DECODE_GRID", grid)
         ws = Q.Workspace(H)
         alice, bob, qx = Q.keygen(H, seeds, q, 0, workspace=ws)
         Q.spec_replays(ws, reset=True)

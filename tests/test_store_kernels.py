@@ -33,16 +33,16 @@ def H(Q, golden_code):
                                       golden_code["chk_idx"])
 
 
-def _use(monkeypatch, kernel):
+def _use(qkd_opt, kernel):
     if kernel == "classic":
-        monkeypatch.setenv("QKD_DECODE_KERNEL", "classic")
+        qkd_opt("QKD_DECODE_KERNEL", "classic")
     else:
-        monkeypatch.delenv("QKD_DECODE_KERNEL", raising=False)
+        qkd_opt("QKD_DECODE_KERNEL", None)
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_trials_config2_golden(Q, H, golden_vectors, monkeypatch, kernel):
-    _use(monkeypatch, kernel)
+def test_trials_config2_golden(Q, H, golden_vectors, monkeypatch, kernel, qkd_opt):
+    _use(qkd_opt, kernel)
     r = Q.run_trials(H, seeds_dev(Q.make_seeds(777, 4096)), 0.02, 0, 50, 100.0, True)
     torch.cuda.synchronize()
     assert (r.iterations.cpu().numpy() == golden_vectors["c2_iters"]).all()
@@ -52,8 +52,8 @@ def test_trials_config2_golden(Q, H, golden_vectors, monkeypatch, kernel):
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("thr,thr_on,max_it", [(100.0, True, 50), (100.0, False, 50), (0.5, True, 7),
                                                (100.0, True, 1), (100.0, True, 2)])
-def test_llr_path(Q, H, oracle_code, oracle_mod, monkeypatch, kernel, thr, thr_on, max_it):
-    _use(monkeypatch, kernel)
+def test_llr_path(Q, H, oracle_code, oracle_mod, monkeypatch, kernel, thr, thr_on, max_it, qkd_opt):
+    _use(qkd_opt, kernel)
     seeds = oracle_mod.seeds(99, 6)
     llr, syn = [], []
     for s in seeds:
@@ -65,8 +65,8 @@ def test_llr_path(Q, H, oracle_code, oracle_mod, monkeypatch, kernel, thr, thr_o
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("q,max_it", [(0.03, 50), (0.5, 6), (0.7, 4), (0.05, 1), (0.05, 2)])
-def test_keys_path_tables(Q, H, oracle_code, monkeypatch, kernel, q, max_it):
-    _use(monkeypatch, kernel)
+def test_keys_path_tables(Q, H, oracle_code, monkeypatch, kernel, q, max_it, qkd_opt):
+    _use(qkd_opt, kernel)
     rng = np.random.default_rng(int(q * 100) + max_it)
     alice = rng.integers(0, 2, (3, 10240))
     bob = alice ^ (rng.random((3, 10240)) < min(q, 0.3))
@@ -74,11 +74,11 @@ def test_keys_path_tables(Q, H, oracle_code, monkeypatch, kernel, q, max_it):
 
 
 @pytest.mark.parametrize("q", [0.05, 0.08])
-def test_sp_f32_same_bits_on_both_kernels(Q, H, monkeypatch, q):
+def test_sp_f32_same_bits_on_both_kernels(Q, H, monkeypatch, q, qkd_opt):
     seeds = seeds_dev(Q.make_seeds(31, 64))
     out = {}
     for kernel in KERNELS:
-        _use(monkeypatch, kernel)
+        _use(qkd_opt, kernel)
         r = Q.run_trials(H, seeds, q, 0, 50, 100.0, True, variant="sp_f32")
         a, b, qq = Q.keygen(H, seeds, q)
         rb = Q.qkd_ldpc(H, a, b, float(qq[0]), 50, 100.0, True, want_bits=True, variant="sp_f32")
@@ -88,13 +88,13 @@ def test_sp_f32_same_bits_on_both_kernels(Q, H, monkeypatch, q):
         assert (x == y).all()
 
 
-def test_split_kernel_is_default_and_classic_selectable(Q, H, monkeypatch):
+def test_split_kernel_is_default_and_classic_selectable(Q, H, monkeypatch, qkd_opt):
     """Both selections run (QKD_PHASE_TIMING off): equal per-frame results on a
     QBER point where frames need many iterations."""
     seeds = seeds_dev(Q.make_seeds(5, 256))
     res = {}
     for kernel in KERNELS:
-        _use(monkeypatch, kernel)
+        _use(qkd_opt, kernel)
         r = Q.run_trials(H, seeds, 0.075, 0, 50, 100.0, True)
         torch.cuda.synchronize()
         res[kernel] = r.iterations.cpu().numpy()

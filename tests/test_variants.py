@@ -102,14 +102,15 @@ def _dev(x, dtype):
     (0.08, 50, 100.0, True, 0.9375, 0.25),
     (0.07, 50, 2.5, True, 1.0 - 1 / 256, 3.0),
 ])
-@pytest.mark.parametrize("store", ["lds", "global"])
+@pytest.mark.parametrize("store", ["split", "lds", "global"])
 def test_minsum_llr_bit_exact(Q, H, ms_model, oracle_mod, monkeypatch, store, q, max_it, thr, thr_on,
-                              scale, offset):
-    """Both min-sum kernels: the frame state in LDS (per-check min1/min2/argmin/
-    signs, the default where it fits) and the per-edge global message store; plain
-    normalised and offset min-sum."""
-    if store == "global":
-        monkeypatch.setenv("QKD_MINSUM_STORE", "global")
+                              scale, offset, qkd_opt):
+    """The three min-sum kernels: the split skeleton (one binary32 slot per
+    edge, all in LDS; the default where it fits), the frame state in LDS
+    (per-check min1/min2/argmin/signs) and the per-edge global message store;
+    plain normalised and offset min-sum."""
+    if store != "split":
+        qkd_opt("QKD_MINSUM_STORE", store)
     A, B, qq = _frames(oracle_mod, q, 48, seed=int(q * 1000) + max_it)
     lp = np.log((1 - qq) / qq)
     llr = np.where(B == 1, -lp, lp)
@@ -129,9 +130,14 @@ def test_minsum_llr_bit_exact(Q, H, ms_model, oracle_mod, monkeypatch, store, q,
 @pytest.mark.parametrize("q,max_it,thr,thr_on,scale", [
     (0.05, 50, 100.0, True, None), (0.08, 50, 100.0, True, 0.875), (0.08, 50, 100.0, True, 0.75),
     (0.07, 6, 2.5, True, 1.0 - 1 / 256), (0.06, 50, 0.0, False, None)])
-def test_minsum_self_corrected_bit_exact(Q, H, ms_model, oracle_mod, q, max_it, thr, thr_on, scale):
-    """Self-corrected min-sum (QKD_MINSUM_SELF_CORRECT, LDS-state kernel) against its
-    specification: erasures of sign-flipped b2c from the second iteration on."""
+@pytest.mark.parametrize("store", ["split", "lds"])
+def test_minsum_self_corrected_bit_exact(Q, H, ms_model, oracle_mod, monkeypatch, store, q, max_it, thr, thr_on,
+                                         scale, qkd_opt):
+    """Self-corrected min-sum (QKD_MINSUM_SELF_CORRECT; the split kernel's per-task
+    ballot words or the LDS-state kernel) against its specification: erasures of
+    sign-flipped b2c from the second iteration on."""
+    if store != "split":
+        qkd_opt("QKD_MINSUM_STORE", store)
     A, B, qq = _frames(oracle_mod, q, 48, seed=int(q * 1000) + 31 + max_it)
     lp = np.log((1 - qq) / qq)
     llr = np.where(B == 1, -lp, lp)
@@ -155,9 +161,9 @@ def test_minsum_self_corrected_bit_exact(Q, H, ms_model, oracle_mod, q, max_it, 
 
 
 @pytest.mark.gpu
-def test_minsum_self_corrected_needs_lds_state(Q, H, monkeypatch):
+def test_minsum_self_corrected_needs_lds_state(Q, H, monkeypatch, qkd_opt):
     """The global-store min-sum has no self-correction: the call fails loudly."""
-    monkeypatch.setenv("QKD_MINSUM_STORE", "global")
+    qkd_opt("QKD_MINSUM_STORE", "global")
     llr = torch.ones((2, 10240), dtype=torch.float64, device="cuda")
     syn = torch.zeros((2, 5231), dtype=torch.uint8, device="cuda")
     with pytest.raises(Q.QkdError):
@@ -165,15 +171,20 @@ def test_minsum_self_corrected_needs_lds_state(Q, H, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_minsum_keys_path_bit_exact(Q, H, ms_model, oracle_mod):
-    """qkd_ldpc (packed-key path, LLR = +-float(log_p)) equals the specification."""
-    A, B, qq = _frames(oracle_mod, 0.07, 48, seed=4242)
+@pytest.mark.parametrize("store,q,offset", [("split", 0.07, None), ("split", 0.02, None), ("split", 0.08, 0.25),
+                                            ("lds", 0.07, None)])
+def test_minsum_keys_path_bit_exact(Q, H, ms_model, oracle_mod, monkeypatch, store, q, offset, qkd_opt):
+    """qkd_ldpc (packed-key path, LLR = +-float(log_p); the split kernel folds
+    its first iteration) equals the specification."""
+    if store != "split":
+        qkd_opt("QKD_MINSUM_STORE", store)
+    A, B, qq = _frames(oracle_mod, q, 48, seed=4242 + int(q * 100))
     r = Q.qkd_ldpc(H, _dev(A, np.uint8), _dev(B, np.uint8), float(qq), 50, 100.0, True,
-                   want_bits=True, variant="minsum")
+                   want_bits=True, variant="minsum", minsum_offset=offset)
     torch.cuda.synchronize()
     lp = np.log((1 - qq) / qq)
     llr = np.where(B == 1, -lp, lp)
-    want_bits, want_it, want_ok = ms_model.decode(llr, ms_model.syndrome(A), scale=0.8125)
+    want_bits, want_it, want_ok = ms_model.decode(llr, ms_model.syndrome(A), scale=0.8125, offset=offset or 0.0)
     assert (r.iterations.cpu().numpy() == want_it).all()
     assert (r.syndromes_match.cpu().numpy() == want_ok).all()
     assert (r.bits.cpu().numpy() == want_bits).all()
@@ -181,10 +192,10 @@ def test_minsum_keys_path_bit_exact(Q, H, ms_model, oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("store", ["lds", "global"])
-def test_minsum_small_codes_bit_exact(Q, dense_codes, monkeypatch, store):
-    if store == "global":
-        monkeypatch.setenv("QKD_MINSUM_STORE", "global")
+@pytest.mark.parametrize("store", ["split", "lds", "global"])
+def test_minsum_small_codes_bit_exact(Q, dense_codes, monkeypatch, store, qkd_opt):
+    if store != "split":
+        qkd_opt("QKD_MINSUM_STORE", store)
     rng = np.random.default_rng(17)
     for name, dense in dense_codes.items():
         m, n = dense.shape

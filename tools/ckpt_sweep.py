@@ -30,7 +30,7 @@ def main():
 
         def run(env):
             for k, v in env.items():
-                os.environ[k] = v
+                Q.set_debug_option(k, v)
             outs = []
             Q.spec_replays(ws, reset=True)
             ts = []
@@ -43,7 +43,7 @@ def main():
                 ts.append(e0.elapsed_time(e1))
                 outs.append(r)
             for k in env:
-                del os.environ[k]
+                Q.set_debug_option(k, None)
             return outs[-1], float(np.median(ts[1:])), Q.spec_replays(ws, reset=True) / 4
         ref, t0, _ = run({"QKD_SPEC_CAP": "0"})
         rit = ref.iterations.cpu().numpy()

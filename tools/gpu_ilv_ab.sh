@@ -14,7 +14,7 @@ for l in $LIBS; do
 done
 for r in $(seq ${REPS:-2}); do
   for l in $LIBS; do
-    QKD_ILV=1 QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=$(libpath $l) timeout -k 10 200 python tools/large_code_bench.py --qber 0.02 \
+    QKD_AMD_DIAGNOSTIC=1 QKD_AMD_LIB=$(libpath $l) timeout -k 10 200 python tools/large_code_bench.py --qber 0.02 --debug-opt QKD_ILV=1 \
       > $O/lc_$l.json 2> $O/lc_$l.err || { tail $O/lc_$l.err; exit 1; }
     python3 -c "import json;d=json.loads(open('$O/lc_$l.json').read().strip().splitlines()[-1]);print('$l', round(d['ms_per_batch'],3))"
   done

@@ -24,7 +24,7 @@ seeds = torch.from_numpy(Q.make_seeds(2024, frames).view(np.int64)).cuda()
 a, b, q = Q.keygen(H, seeds, qb)
 out = {}
 for mode in ("1", "0"):
-    os.environ["QKD_ILV"] = mode
+    Q.set_debug_option("QKD_ILV", mode)
     r = Q.qkd_ldpc(H, a, b, float(q[0]), 50)
     torch.cuda.synchronize()
     out[mode] = r

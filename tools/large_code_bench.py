@@ -20,7 +20,12 @@ ap.add_argument("--n", type=int, default=40000)
 ap.add_argument("--frames", type=int, default=4096)
 ap.add_argument("--qber", type=float, default=0.03)
 ap.add_argument("--variant", default="sp_f64")
+ap.add_argument("--phase-timing", action="store_true", help="per-phase shader clocks (QKD_PHASE_TIMING option)")
+ap.add_argument("--debug-opt", action="append", default=[], metavar="NAME=VALUE",
+                help="a library debug option (qkd_debug_set_option), process-wide; repeatable")
 args = ap.parse_args()
+for kv in args.debug_opt + (["QKD_PHASE_TIMING=1"] if args.phase_timing else []):
+    Q.set_debug_option(kv.partition("=")[0], kv.partition("=")[2])
 m, cp, ci = regular_code(args.n, seed=11)
 H = Q.HMatrix.from_check_lists(args.n, cp, ci)
 seeds = torch.from_numpy(Q.make_seeds(777, args.frames).view(np.int64)).cuda()
@@ -42,7 +47,7 @@ hist = np.bincount(it).tolist()
 lock = {str(g): float(it[: len(it) // g * g].reshape(-1, g).max(axis=1).sum() * g / it[: len(it) // g * g].sum())
         for g in (2, 4, 8, 16)}
 extra = {}
-if os.environ.get("QKD_PHASE_TIMING"):
+if args.phase_timing:
     # the last call's summed shader-clock cycles per phase (the interleaved
     # decoder: check, bit, syndrome test + outcomes, refill)
     cyc = np.zeros(7, dtype=np.uint64)

@@ -4,6 +4,6 @@
 set -u
 mkdir -p gpurun_out/lc
 for g in 256 192 128 96 64; do
-  QKD_DECODE_GRID=$g timeout -k 10 120 python tools/large_code_bench.py --qber 0.02 > gpurun_out/lc/grid_$g.json 2>gpurun_out/lc/grid_$g.err || { echo "grid $g failed"; tail -3 gpurun_out/lc/grid_$g.err; exit 1; }
+  timeout -k 10 120 python tools/large_code_bench.py --qber 0.02 --debug-opt QKD_DECODE_GRID=$g > gpurun_out/lc/grid_$g.json 2>gpurun_out/lc/grid_$g.err || { echo "grid $g failed"; tail -3 gpurun_out/lc/grid_$g.err; exit 1; }
   echo "grid $g $(cat gpurun_out/lc/grid_$g.json)"
 done
