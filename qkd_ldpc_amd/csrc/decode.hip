@@ -1628,7 +1628,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
         c->n <= kMaxBitsSplit && c->m <= kMaxChecksSplit && c->max_dc <= 8) {
         // (check degree <= 8: the additive mask table, seg_weight_entries)
         const SplitLds Lm(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, c->max_dc <= 4 ? 4 : c->max_dc <= 6 ? 6 : 8,
-                          0, a.ms_sc ? 2 * c->n_tasks : 0, 4, kLdsBytesMax);
+                          0, a.ms_sc ? 2 * c->n_tasks + (c->n + 63) / 64 : 0, 4, kLdsBytesMax);
         if (Lm.S >= (uint32_t)((size_t)c->max_dv * c->n_pad) && Lm.bytes <= kLdsBytesMax)
             rule = a.ms_sc ? kRuleMinSumSplitSc : kRuleMinSumSplit;
     }
@@ -1667,8 +1667,9 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
         // (QKD_FOLD_TABLE=0: the per-bit form; tests compare the two)
         if (const DbgOpt e = debug_option(ws, "QKD_FOLD_TABLE")) if (e.as_int() == 0) a.ftab_entries = 0;
         if (debug_option(ws, "QKD_SPEC_POLICY").is("always")) a.spec_always = 1u;
-        // (self-corrected min-sum: its previous-b2c ballot words in the ftab region)
-        if (rule == kRuleMinSumSplitSc) a.ftab_entries = 2 * c->n_tasks;
+        // (self-corrected min-sum: its previous-b2c ballot words and the
+        // frame's Bob words in the ftab region)
+        if (rule == kRuleMinSumSplitSc) a.ftab_entries = 2 * c->n_tasks + (c->n + 63) / 64;
         const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, a.ftab_entries, esz,
                          budget);
         // (the binary32 rule's kernel keeps every slot in LDS: SplitStore<float, true>)
@@ -2065,11 +2066,10 @@ static qkd_status decode_keys(const qkd_code* c, qkd_workspace* ws, size_t n_fra
     // first-iteration message magnitudes by check degree (first_check_phase)
     // (the binary32 rule folds on the device, decode_split_kernel; not at
     // log_p = 0, where Bob's 1 bits give -0.0, not negative)
-    // (min-sum folds on the device too, decode_split_kernel, without the
-    // self-correction, whose first check phase records every b2c)
+    // (min-sum folds on the device too, decode_split_kernel)
     a.first_table = (c->max_dc <= kFirstTableDeg &&
-                     (rule_of(flags) == kRuleSp64 || (rule_of(flags) == kRuleSp32 && a.log_p != 0.0) ||
-                      (rule_of(flags) == kRuleMinSum && !(flags & QKD_MINSUM_SELF_CORRECT) && a.log_p != 0.0)))
+                     (rule_of(flags) == kRuleSp64 ||
+                      ((rule_of(flags) == kRuleSp32 || rule_of(flags) == kRuleMinSum) && a.log_p != 0.0)))
                         ? 1 : 0;
     if (a.first_table) {
         const double T = std::fabs(qkdm::tanh_flat(a.log_p / 2.0));

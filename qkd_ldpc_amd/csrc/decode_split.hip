@@ -400,11 +400,18 @@ __device__ __forceinline__ void sp32_check_phase(const uint2* __restrict__ plan,
 // differs from the edge's previous b2c, both nonzero, is erased to 0 before
 // the rule. The previous b2c of every edge is two ballot words per task in
 // LDS (scw[2 t]: negative, scw[2 t + 1]: nonzero), read and rewritten by the
-// task's wave; sc_on is false in the frame's first check phase (no previous).
+// task's wave. sc_mode: 0 the frame's first check phase (no previous b2c), 1
+// the previous b2c from scw, 2 the check phase after the folded first
+// iteration, whose b2c were the channel LLRs: negative iff Bob's bit of the
+// edge (bwl, the frame's key words) differs from the sign of log_p (lsign),
+// nonzero (the fold needs log_p != 0); the edge's bit is its slot index
+// (the plan word's LDS address, msg the first slot's) modulo n_pad.
 template <bool CLAMP, int DC, bool SC, bool OFF, typename MS>
 __device__ __forceinline__ void ms_split_check_phase(const uint2* __restrict__ plan, const MS& ms, float* row,
-                                                     const float* mtab, uint64_t* scw, bool sc_on, int n_tasks,
-                                                     float thr, float scale, float off, int wave, int lane) {
+                                                     const float* mtab, uint64_t* scw, int sc_mode,
+                                                     const uint64_t* bwl, uint32_t msg, uint32_t n_pad,
+                                                     uint32_t lsign, int n_tasks, float thr, float scale, float off,
+                                                     int wave, int lane) {
     static_assert(DC <= 8, "min-sum split buckets: check degree <= 8 (the mask table)");
     typedef __attribute__((address_space(3))) float LdsF;
     constexpr int NW = kDecodeBlock / 64;
@@ -418,11 +425,21 @@ __device__ __forceinline__ void ms_split_check_phase(const uint2* __restrict__ p
     auto slot = [](uint2 p) -> LdsF* { return reinterpret_cast<LdsF*>((size_t)p.x); };
     // b2c of task tt's edge after the self-correction; records it as the
     // edge's previous b2c
-    auto input = [&](float x, int tt) -> float {
+    auto input = [&](float x, uint2 w, int tt) -> float {
         if constexpr (SC) {
-            if (sc_on) {
-                const uint64_t pneg = scw[2 * tt], pnz = scw[2 * tt + 1];
-                const bool er = ((pnz >> lane) & 1ull) && x != 0.0f && (x < 0.0f) != (((pneg >> lane) & 1ull) != 0);
+            if (sc_mode != 0) {
+                bool pn, pz;      // the previous b2c: negative, nonzero
+                if (sc_mode == 1) {
+                    pn = ((scw[2 * tt] >> lane) & 1ull) != 0;
+                    pz = ((scw[2 * tt + 1] >> lane) & 1ull) != 0;
+                } else {
+                    uint32_t i = (w.x - msg) >> 2;          // (bit degree <= 3: bit_code)
+                    i = i >= n_pad ? i - n_pad : i;
+                    i = i >= n_pad ? i - n_pad : i;
+                    pn = ((uint32_t)(bwl[i >> 6] >> (i & 63u)) & 1u) != lsign;
+                    pz = true;
+                }
+                const bool er = pz && x != 0.0f && (x < 0.0f) != pn;
                 x = er ? 0.0f : x;
             }
             const uint64_t nneg = __ballot(x < 0.0f), nnz = __ballot(x != 0.0f);
@@ -436,7 +453,7 @@ __device__ __forceinline__ void ms_split_check_phase(const uint2* __restrict__ p
     uint2 wt = plan_word(prs, t, lane);
     uint2 wn = plan_word(prs, t + NW, lane);
     uint2 wnn = plan_word(prs, t + 2 * NW, lane);
-    float xt = input(*slot(wt), t);
+    float xt = input(*slot(wt), wt, t);
     row[lane] = __builtin_fabsf(xt);
     uint64_t sgn_t = __ballot(xt < 0.0f);
     bool neg_t = xt < 0.0f;
@@ -465,7 +482,7 @@ __device__ __forceinline__ void ms_split_check_phase(const uint2* __restrict__ p
         if (t >= n_tasks) return false;
         // the next task's row (after this task's row reads: a wave's LDS
         // accesses complete in order)
-        const float xc = input(x_n, t);
+        const float xc = input(x_n, w_n, t);
         row[lane] = __builtin_fabsf(xc);
         sgn_t = __ballot(xc < 0.0f);
         neg_t = xc < 0.0f;
@@ -1127,7 +1144,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     constexpr bool MSR = RULE == kRuleMinSumSplit || RULE == kRuleMinSumSplitSc;   // min-sum rules
     constexpr bool MSC = RULE == kRuleMinSumSplitSc;
     constexpr bool F32 = RULE != kRuleSp64;       // binary32 slots, all in LDS
-    constexpr bool FOLDS = MODE == kModeKeys && (RULE == kRuleSp64 || RULE == kRuleSp32 || RULE == kRuleMinSumSplit);
+    constexpr bool FOLDS = MODE == kModeKeys && (RULE == kRuleSp64 || RULE == kRuleSp32 || MSR);
     constexpr bool TABLES = MODE == kModeKeys && RULE == kRuleSp64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const DeviceCode& c = a.code;
@@ -1200,7 +1217,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             ctab[tid] = (double)v;
         }
     }
-    if constexpr (RULE == kRuleMinSumSplit && FOLDS) {
+    if constexpr (MSR && FOLDS) {
         // the min-sum rule's first messages (every |b2c| = |float(log_p)|):
         // scale * |log_p| - off, floored at 0, clamped, for every degree >= 2;
         // degree 1 has no other edge (min over nothing: +inf)
@@ -1212,8 +1229,10 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
         }
     }
     // self-corrected min-sum: the previous b2c of each edge, two ballot words
-    // per task (ms_split_check_phase), in the ftab region (host: ftab_entries)
+    // per task (ms_split_check_phase), then the frame's Bob words (keys path),
+    // in the ftab region (host: ftab_entries)
     uint64_t* const scw = MSC ? reinterpret_cast<uint64_t*>(smem + L.ftab) : nullptr;
+    uint64_t* const bwl = MSC ? scw + 2 * c.n_tasks : nullptr;
     if (tab2_on) {
         __syncthreads();
         second_table_fill<CLAMP>(c, ctab, a.log_p, a.thr, tab2, a.tab2_entries);
@@ -1307,6 +1326,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 const uint64_t av = ka ? a.alice_w[(size_t)f * a.words + q] : 0ull;
                 w[q] = bv;
                 aw[q] = av;
+                if constexpr (MSC) bwl[q] = bv;
             }
             const uint32_t* sy = a.synw + (size_t)f * 2 * m_words;
             for (int q = tid; q < m_words; q += kDecodeBlock) {
@@ -1431,12 +1451,15 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 }
             } else if (!folded) {
                 if constexpr (MSR) {
+                    const int sc_mode = it == 0 ? 0 : (fold1 && it == 1 ? 2 : 1);
                     if (a.ms_offset > 0.0f)
-                        ms_split_check_phase<CLAMP, DC, MSC, true>(plan, ms, row, wtab, scw, it > 0, n_tasks,
-                                                                   (float)thr, a.ms_scale, a.ms_offset, wave, lane);
+                        ms_split_check_phase<CLAMP, DC, MSC, true>(plan, ms, row, wtab, scw, sc_mode, bwl,
+                                                                   (uint32_t)L.msg, n_pad, lsign, n_tasks, (float)thr,
+                                                                   a.ms_scale, a.ms_offset, wave, lane);
                     else
-                        ms_split_check_phase<CLAMP, DC, MSC, false>(plan, ms, row, wtab, scw, it > 0, n_tasks,
-                                                                    (float)thr, a.ms_scale, a.ms_offset, wave, lane);
+                        ms_split_check_phase<CLAMP, DC, MSC, false>(plan, ms, row, wtab, scw, sc_mode, bwl,
+                                                                    (uint32_t)L.msg, n_pad, lsign, n_tasks, (float)thr,
+                                                                    a.ms_scale, a.ms_offset, wave, lane);
                 } else if constexpr (RULE == kRuleSp32)
                     sp32_check_phase<CLAMP, DC>(c.plan_slot, tsyn, ms, row, wtab, n_tasks, n_pad, thr, wave, lane);
                 else if (TABLES && it == 1 && tab2_on)
