@@ -1644,10 +1644,20 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
     // decode_kernel (A/B measurements, tests). Trace mode records the classic
     // kernel's store.
     const bool msr = rule == kRuleMinSumSplit || rule == kRuleMinSumSplitSc;
-    if ((rule == kRuleSp64 || rule == kRuleSp32 || msr) && !classic && !a.trace && c->n <= kMaxBitsSplit &&
+    // codes past kMaxBitsSplit (up to kMaxBitsSplitLong): only the
+    // frame-interleaved decoder and its exact hand-off kernel (LONG) take
+    // them, on the keys path with the split view's arrays; otherwise the
+    // classic kernel below
+    const bool long_code = c->n > kMaxBitsSplit;
+    const bool long_ok = rule == kRuleSp64 && mode == kModeKeys && c->n <= kMaxBitsSplitLong && c->d_ilv_slots &&
+                         c->max_dc <= 16;
+    if ((rule == kRuleSp64 || rule == kRuleSp32 || msr) && !classic && !a.trace && (!long_code || long_ok) &&
         c->m <= kMaxChecksSplit) {
+        // (a long code falls back to the classic kernel with the arguments as given)
+        const DecodeArgs a_in = a;
         int sdc = 0;
-        DecodeFn sfn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &sdc);
+        DecodeFn sfn = long_code ? pick_split_long(a.clamp_on != 0, c->max_dc, &sdc)
+                                 : pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &sdc);
         const int esz = rule == kRuleSp64 ? 8 : 4;
         // diagnostic: QKD_SPLIT_BUDGET lowers the LDS budget (fewer LDS slots)
         size_t budget = kLdsBytesMax;
@@ -1670,6 +1680,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
         // (self-corrected min-sum: its previous-b2c ballot words and the
         // frame's Bob words in the ftab region)
         if (rule == kRuleMinSumSplitSc) a.ftab_entries = 2 * c->n_tasks + (c->n + 63) / 64;
+        // (the long-code hand-off kernel: the frame's Bob words there)
+        if (long_code) a.ftab_entries = std::max(a.ftab_entries, (c->n + 63) / 64);
         const SplitLds L(c->n_pad, (c->n + 63) / 64, c->m, c->max_dv, sdc, a.tab2_entries, a.ftab_entries, esz,
                          budget);
         // (the binary32 rule's kernel keeps every slot in LDS: SplitStore<float, true>)
@@ -1724,15 +1736,18 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             a.replay_count = ws->counter + 1;
             a.spec_replays = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws->counter) + 120);
             if (spec) {
-                int xdc = 0, sgrid = 0;
-                DecodeFn xfn = pick_split_spec(mode, c->max_dc, ckpt, &xdc);
-                if (xdc != sdc)      // (the layout and the encoded plan are the bucket's)
-                    return set_error(QKD_ERR_UNSUPPORTED, "speculative kernel bucket %d != %d", xdc, sdc);
-                s = decode_grid(c, xfn, L.bytes, &sgrid);
-                if (s != QKD_OK) return s;
-                sfn = xfn;
-                grid = std::min(sgrid, grid);
-                if (ckpt) {
+                // (a long code: the interleaved decoder speculates; no split speculation)
+                if (!long_code) {
+                    int xdc = 0, sgrid = 0;
+                    DecodeFn xfn = pick_split_spec(mode, c->max_dc, ckpt, &xdc);
+                    if (xdc != sdc)      // (the layout and the encoded plan are the bucket's)
+                        return set_error(QKD_ERR_UNSUPPORTED, "speculative kernel bucket %d != %d", xdc, sdc);
+                    s = decode_grid(c, xfn, L.bytes, &sgrid);
+                    if (s != QKD_OK) return s;
+                    sfn = xfn;
+                    grid = std::min(sgrid, grid);
+                }
+                if (ckpt && !long_code) {
                     // one saved message store per resident workgroup
                     const size_t need = (size_t)grid * slots;
                     if (ws->ckpt_slots < need) {
@@ -1777,8 +1792,10 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             // (the target syndrome words in LDS when the three arrays fit, else
             // in global memory: measured 30 % slower at N = 40,000, where
             // they fit, and twice as fast as the split kernel at 60,000)
+            // (then also the uncertainty words, for M past ~37,000)
             const bool tsg = IlvLds(c->m, false).bytes > kLdsBytesMax;
-            const IlvLds IL(c->m, tsg);
+            const bool ug = tsg && IlvLds(c->m, true).bytes > kLdsBytesMax;
+            const IlvLds IL(c->m, tsg, ug);
             bool ilv = mode == kModeKeys && spec && !ckpt && !a.bits_out && a.first_table && c->d_ilv_slots &&
                        IL.bytes <= kLdsBytesMax;
             bool ilv_forced = false;
@@ -1794,10 +1811,11 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             // target syndrome words: (M + 1) / 2 words, in doubles)
             // rounded to 512 bytes: every workgroup's lines start on a cache
             // line (an unaligned stride splits each line access in two)
+            // (and, ug, their uncertainty words as many again)
             const size_t istride = (slots * kIlvCols + (size_t)((c->n + 63) / 64) * kIlvCols * 2 +
-                                    ((size_t)(c->m + 1) / 2 + 1) / 2 + 63) & ~(size_t)63;
+                                    (ug ? 2 : 1) * (((size_t)(c->m + 1) / 2 + 1) / 2) + 63) & ~(size_t)63;
             if (ilv) {
-                ifn = pick_ilv(c->ilv_rs, c->max_dc, tsg);
+                ifn = pick_ilv(c->ilv_rs, c->max_dc, tsg, ug);
                 QKD_HIP(hipFuncSetAttribute((const void*)ifn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)IL.bytes));
                 int per_cu = 0;
                 QKD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ifn, kIlvBlock, IL.bytes));
@@ -1824,6 +1842,11 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                         ws->ilv_elems = need;
                     }
                 }
+            }
+            // (a long code the interleaved decoder does not take: the classic kernel)
+            if (long_code && !ilv) {
+                a = a_in;
+                goto classic_path;
             }
             if (ilv) {
                 if (ws->fb_frames < a.n_frames) {
@@ -1872,7 +1895,8 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
                 af.spec_always = 1;
                 af.phase = nullptr;       // (QKD_PHASE_TIMING: the interleaved kernel's phases)
                 int xdc = 0;
-                DecodeFn ffn = pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &xdc);
+                DecodeFn ffn = long_code ? pick_split_long(a.clamp_on != 0, c->max_dc, &xdc)
+                                         : pick_split_decode(mode, rule, a.clamp_on != 0, c->max_dc, &xdc);
                 if (xdc != sdc)
                     return set_error(QKD_ERR_UNSUPPORTED, "exact split kernel bucket %d != %d", xdc, sdc);
                 // (the interleaved launch's error is read once and carried to
@@ -1892,6 +1916,7 @@ static qkd_status launch_decode(const qkd_code* c, qkd_workspace* ws, DecodeArgs
             return QKD_OK;
         }
     }
+classic_path:
     const bool gt = decode_needs_gt(c, rule, a.tab2_entries);
     if (gt) {                                     // large code: no per-bit LDS tables
         a.first_table = 0;

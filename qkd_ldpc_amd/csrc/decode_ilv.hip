@@ -81,8 +81,10 @@ __device__ __forceinline__ uint32_t fold_groups(uint64_t b) {
 // RS: the row stride of DeviceCode::ilv_slots; DM: the largest check degree
 // rounded up to even (the register arrays' size); TG: the target syndrome
 // words in global memory (IlvLds: codes whose three LDS syndrome arrays would
-// not fit)
-template <int RS, int DM, bool TG>
+// not fit); UG (with TG): the uncertainty words there too, after the target
+// words (codes past M ~ 37,000: kept by L2 atomics, read and cleared by
+// exchange)
+template <int RS, int DM, bool TG, bool UG = false>
 __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     static_assert(DM <= RS && DM % 2 == 0, "degree bucket");
     using qkds::f2;
@@ -92,10 +94,10 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     const int lane = tid & 63;
     const uint32_t col = (uint32_t)tid & (kIlvCols - 1);
     const int grp = tid / kIlvCols;
-    const IlvLds L(c.m, TG);
+    static_assert(TG || !UG, "global uncertainty words follow global target words");
+    const IlvLds L(c.m, TG, UG);
     const uint32_t mw2 = (uint32_t)(c.m + 1) >> 1;
     uint32_t* xsyn = reinterpret_cast<uint32_t*>(smem + L.xsyn);
-    uint32_t* xunc = reinterpret_cast<uint32_t*>(smem + L.xunc);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + L.ctl);
     double* ctab = reinterpret_cast<double*>(smem + L.ctab);
     uint32_t* ilv_ring = reinterpret_cast<uint32_t*>(smem + L.ring);
@@ -112,6 +114,8 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     // phase then loads each check's word with its lines)
     uint32_t* const tsyn = TG ? reinterpret_cast<uint32_t*>(keyi + (size_t)a.words * kIlvCols)
                               : reinterpret_cast<uint32_t*>(smem + L.tsyn);
+    // (the region rounds the target words up to whole doubles)
+    uint32_t* const xunc = UG ? tsyn + ((mw2 + 1u) & ~1u) : reinterpret_cast<uint32_t*>(smem + L.xunc);
     // The lines through a buffer descriptor: a line index of ~0 (an edge past
     // the check's degree, a row past the bit's) gives an offset past the
     // region, which loads 0 and drops the store -- no branch around any
@@ -133,7 +137,10 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     for (uint32_t w = (uint32_t)tid; w < mw2; w += kIlvBlock) {
         tsyn[w] = 0;
         xsyn[w] = 0;
-        xunc[w] = 0;
+        if constexpr (UG)
+            __hip_atomic_store(xunc + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            xunc[w] = 0;
     }
     if (tid < kIlvCtlWords) ctl[tid] = 0;
     __syncthreads();
@@ -511,12 +518,12 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
         // and a check whose parity is uncertain; xsyn / xunc cleared
         uint32_t mis = 0, un = 0;
         for (uint32_t w = (uint32_t)tid; w < mw2; w += kIlvBlock) {
-            const uint32_t u = xunc[w];
+            const uint32_t u = UG ? atomicExch(xunc + w, 0u) : xunc[w];
             const uint32_t d = (xsyn[w] ^ tsyn[w]) & ~u;
             mis |= d | (d >> 16);
             un |= u | (u >> 16);
             xsyn[w] = 0;
-            xunc[w] = 0;
+            if constexpr (!UG) xunc[w] = 0;
         }
         mis &= 0xffffu;
         un &= 0xffffu;
@@ -596,16 +603,17 @@ __global__ __launch_bounds__(kIlvBlock) void decode_ilv_kernel(DecodeArgs a) {
     }
 }
 
-template <bool TG>
+template <bool TG, bool UG>
 static DecodeFn pick_ilv_dc(int rs, int max_dc) {
-    if (rs > 8) return decode_ilv_kernel<16, 16, TG>;
-    if (max_dc <= 4) return decode_ilv_kernel<8, 4, TG>;
-    if (max_dc <= 6) return decode_ilv_kernel<8, 6, TG>;
-    return decode_ilv_kernel<8, 8, TG>;
+    if (rs > 8) return decode_ilv_kernel<16, 16, TG, UG>;
+    if (max_dc <= 4) return decode_ilv_kernel<8, 4, TG, UG>;
+    if (max_dc <= 6) return decode_ilv_kernel<8, 6, TG, UG>;
+    return decode_ilv_kernel<8, 8, TG, UG>;
 }
 
-DecodeFn pick_ilv(int rs, int max_dc, bool tsyn_global) {
-    return tsyn_global ? pick_ilv_dc<true>(rs, max_dc) : pick_ilv_dc<false>(rs, max_dc);
+DecodeFn pick_ilv(int rs, int max_dc, bool tsyn_global, bool xunc_global) {
+    if (xunc_global) return pick_ilv_dc<true, true>(rs, max_dc);
+    return tsyn_global ? pick_ilv_dc<true, false>(rs, max_dc) : pick_ilv_dc<false, false>(rs, max_dc);
 }
 
 }  // namespace qkd

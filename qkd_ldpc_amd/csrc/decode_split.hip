@@ -1133,8 +1133,13 @@ __device__ __forceinline__ uint32_t region_of_block() {
 #else
 #define QKD_SPLIT_BOUNDS __launch_bounds__(kDecodeBlock)
 #endif
-template <int MODE, int RULE, int DC, bool CLAMP, int SPEC>
+// LONG: codes past kMaxBitsSplit bits (up to kMaxBitsSplitLong), the exact
+// keys-path kernel only (the frame-interleaved decoder's hand-offs): Bob's
+// bits of rounds 64 and up come from the frame's key words kept in LDS (the
+// ftab region, DecodeArgs::ftab_entries >= words) instead of bobmask.
+template <int MODE, int RULE, int DC, bool CLAMP, int SPEC, bool LONG = false>
 __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
+    static_assert(!LONG || (MODE == kModeKeys && RULE == kRuleSp64 && SPEC == 0), "long codes: exact keys path");
     using T = typename RuleMsg<RULE>::T;
     // QKD path: the first check phase folds into the first bit phase for both
     // sum-product rules (every b2c is +-log_p, so every message is +-C_d:
@@ -1232,7 +1237,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     // per task (ms_split_check_phase), then the frame's Bob words (keys path),
     // in the ftab region (host: ftab_entries)
     uint64_t* const scw = MSC ? reinterpret_cast<uint64_t*>(smem + L.ftab) : nullptr;
-    uint64_t* const bwl = MSC ? scw + 2 * c.n_tasks : nullptr;
+    uint64_t* const bwl = MSC ? scw + 2 * c.n_tasks : (LONG ? reinterpret_cast<uint64_t*>(smem + L.ftab) : nullptr);
     if (tab2_on) {
         __syncthreads();
         second_table_fill<CLAMP>(c, ctab, a.log_p, a.thr, tab2, a.tab2_entries);
@@ -1326,7 +1331,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 const uint64_t av = ka ? a.alice_w[(size_t)f * a.words + q] : 0ull;
                 w[q] = bv;
                 aw[q] = av;
-                if constexpr (MSC) bwl[q] = bv;
+                if constexpr (MSC || LONG) bwl[q] = bv;
             }
             const uint32_t* sy = a.synw + (size_t)f * 2 * m_words;
             for (int q = tid; q < m_words; q += kDecodeBlock) {
@@ -1352,7 +1357,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                     l = (T)a.llr[(size_t)f * c.n + c.perm[i]];
                 } else {
                     const uint32_t bb = (uint32_t)((bw[i >> 6] >> (i & 63)) & 1u);
-                    bobmask |= (uint64_t)bb << r;
+                    if (!LONG || r < 64) bobmask |= (uint64_t)bb << r;
                     l = bb ? -llr_p : llr_p;
                 }
                 if (!fold1) {
@@ -1367,6 +1372,12 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             if (tid == 0) ms.st((uint32_t)c.n, (T)0);
         };
         init_slots(spec0);
+        // Bob's bit of this thread's round r (LONG: past round 63 from LDS)
+        auto bob_r = [&](int r) -> uint32_t {
+            if constexpr (LONG)
+                if (r >= 64) return (uint32_t)(bwl[(r * kDecodeBlock >> 6) + wave] >> lane) & 1u;
+            return (uint32_t)(bobmask >> r) & 1u;
+        };
         // running syndrome (kRunSyn): the last decision = Bob's key (keys path,
         // the words staged above) or 0 (LLR path), and xsyn = H * it: from
         // frame_syn's words, q_j = s_j ^ (H bob)_j ^ (deg_j & sign(log_p))
@@ -1545,11 +1556,11 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                     const int deg = dg[u];
                     T acc;
                     if (MODE == kModeLlr) acc = ok ? (T)a.llr[(size_t)f * c.n + c.perm[i]] : (T)0;
-                    else acc = ((uint32_t)(bobmask >> r) & 1u) ? -llr_p : llr_p;
+                    else acc = bob_r(r) ? -llr_p : llr_p;
                     if constexpr (FOLDS) if (folded && ok) {
                         // fold_first_message: message of the k-th check j of bit i is
                         // +-C_{d_j} with sign = sign(P_j) ^ sign(LLR_i) (first_check_phase)
-                        const uint32_t sgi = ((uint32_t)(bobmask >> r) & 1u) ^ lsign;
+                        const uint32_t sgi = bob_r(r) ^ lsign;
 #pragma unroll
                         for (int k = 0; k < kDvUnroll; ++k) {
                             if (k < deg) {
@@ -1582,7 +1593,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                     if (TABLES && folded && tab2_on) {
                         // second_table_index: Bob's bit and the signs of the first
                         // messages; the slot of row k keeps the index of its entry
-                        uint32_t code = (uint32_t)(bobmask >> r) & 1u;
+                        uint32_t code = bob_r(r);
 #pragma unroll
                         for (int k = 0; k < kTab2MaxDv; ++k)
                             if (k < deg) code |= ((uint32_t)qkdm::hi32(v[u][k]) >> 31) << (1 + k);
@@ -2142,6 +2153,19 @@ static DecodeFn pick_split_rule(int rule, bool clamp, int max_dc, int* dc) {
     if (rule == kRuleMinSumSplitSc) return pick_split_ms<MODE, kRuleMinSumSplitSc>(clamp, max_dc, dc);
     if (rule == kRuleSp32) return pick_split_clamp<MODE, kRuleSp32>(clamp, max_dc, dc);
     return pick_split_clamp<MODE, kRuleSp64>(clamp, max_dc, dc);
+}
+
+// the exact keys-path kernel for codes past kMaxBitsSplit (LONG)
+DecodeFn pick_split_long(bool clamp, int max_dc, int* dc) {
+    if (max_dc <= 4) { *dc = 4; return clamp ? decode_split_kernel<kModeKeys, kRuleSp64, 4, true, 0, true>
+                                             : decode_split_kernel<kModeKeys, kRuleSp64, 4, false, 0, true>; }
+    if (max_dc <= 6) { *dc = 6; return clamp ? decode_split_kernel<kModeKeys, kRuleSp64, 6, true, 0, true>
+                                             : decode_split_kernel<kModeKeys, kRuleSp64, 6, false, 0, true>; }
+    if (max_dc <= 8) { *dc = 8; return clamp ? decode_split_kernel<kModeKeys, kRuleSp64, 8, true, 0, true>
+                                             : decode_split_kernel<kModeKeys, kRuleSp64, 8, false, 0, true>; }
+    *dc = 16;
+    return clamp ? decode_split_kernel<kModeKeys, kRuleSp64, 16, true, 0, true>
+                 : decode_split_kernel<kModeKeys, kRuleSp64, 16, false, 0, true>;
 }
 
 DecodeFn pick_split_decode(int mode, int rule, bool clamp, int max_dc, int* dc) {

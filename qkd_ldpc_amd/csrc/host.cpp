@@ -377,12 +377,14 @@ static qkd_status build_code(qkd_code* c, int32_t n, int32_t m, const int32_t* c
                           hipMemcpyHostToDevice));
         QKD_HIP(hipMemcpy(c->d_pat_deg, c->pat_deg.data(), c->pat_deg.size(), hipMemcpyHostToDevice));
     }
-    // The split kernels' data (decode_split.hip), only for codes they take
-    // (N <= kMaxBitsSplit, M <= kMaxChecksSplit; the launcher checks the same):
-    // larger codes run the classic kernel on the original order, so the
-    // internal bit order (its bank pass searches up to 200k moves) and the
-    // internal-order arrays are neither computed nor uploaded for them.
-    const bool split = n <= kMaxBitsSplit && m <= kMaxChecksSplit;
+    // The split kernels' data (decode_split.hip, decode_ilv.hip), only for
+    // codes they take (N <= kMaxBitsSplitLong, M <= kMaxChecksSplit; past
+    // kMaxBitsSplit only the frame-interleaved decoder and its exact hand-off
+    // kernel; the launcher checks the same): larger codes run the classic
+    // kernel on the original order, so the internal bit order (its bank pass
+    // searches up to 200k moves) and the internal-order arrays are neither
+    // computed nor uploaded for them.
+    const bool split = n <= kMaxBitsSplitLong && m <= kMaxChecksSplit;
     std::vector<int32_t> perm(n), inv(n, -1);
     if (split) {
     // the split kernels' internal bit order (internal_bit_order)

@@ -199,14 +199,17 @@ constexpr int kRingStage = 16;
 struct IlvLds {
     size_t tsyn, xsyn, xunc, ctl, ctab, ring, bytes;
     // tsyn_global: the target syndrome words in the workgroup's global region
-    // instead (decode_ilv_kernel's TG), for codes whose three arrays do not fit
-    __host__ __device__ IlvLds(int m, bool tsyn_global) {
+    // instead (decode_ilv_kernel's TG), for codes whose three arrays do not
+    // fit; xunc_global (UG, with TG): the uncertainty words there too (M past
+    // ~37,000: only the XOR-built syndrome stays in LDS)
+    __host__ __device__ IlvLds(int m, bool tsyn_global, bool xunc_global = false) {
         const size_t mw2 = (size_t)(m + 1) / 2;
         const size_t k = tsyn_global ? 0 : 1;
+        const size_t u = xunc_global ? 0 : 1;
         tsyn = 0;
         xsyn = k * mw2 * 4;
         xunc = (k + 1) * mw2 * 4;
-        ctl = ((k + 2) * mw2 * 4 + 15) & ~(size_t)15;
+        ctl = ((k + 1 + u) * mw2 * 4 + 15) & ~(size_t)15;
         ctab = ctl + (size_t)kIlvCtlWords * 4;
         ring = ctab + (size_t)(kFirstTableDeg + 1) * 8;
         bytes = ring + (size_t)(kIlvBlock / kIlvCols) * 4 * kRingStage * 4;
@@ -642,12 +645,15 @@ using DecodeFn = void (*)(DecodeArgs);
 // decode_split.hip: the split-store kernel for (mode, rule in {kRuleSp64,
 // kRuleSp32}, clamp, check-degree bucket); *dc receives the bucket.
 DecodeFn pick_split_decode(int mode, int rule, bool clamp, int max_dc, int* dc);
+// the exact keys-path split kernel for codes past kMaxBitsSplit bits (up to
+// kMaxBitsSplitLong; check degree <= 16): the interleaved decoder's hand-offs
+DecodeFn pick_split_long(bool clamp, int max_dc, int* dc);
 // The speculative kernel (binary64 rule, clamp on) for a mode; ckpt: the
 // checkpointed variant (keys path: exact iterations first, interval ones from
 // a checkpoint once few checks are unsatisfied).
 DecodeFn pick_split_spec(int mode, int max_dc, bool ckpt, int* dc);
 // the frame-interleaved decoder (decode_ilv.hip) for check-row stride rs (8 or 16)
-DecodeFn pick_ilv(int rs, int max_dc, bool tsyn_global);
+DecodeFn pick_ilv(int rs, int max_dc, bool tsyn_global, bool xunc_global = false);
 // decode_split.hip, kModeKeys: the kernels around the split decoder.
 // Before: a.synw from the packed keys. After: key_ok / bits_out from a.zout.
 // gather: the gather kernel instead of the bit-sliced one; pack_first: byte

@@ -38,6 +38,9 @@ constexpr int kMaxBitsLds = 20480;
 // The split-store kernels (decode_split.hip): Bob's bits of a thread's
 // bit-phase rounds in one 64-bit register, 64 rounds of kDecodeBlock bits
 constexpr int kMaxBitsSplit = 64 * kDecodeBlock;
+// longer codes (the frame-interleaved decoder and its exact hand-off kernel,
+// decode_split_kernel<..., LONG>): the split view's arrays exist up to this
+constexpr int kMaxBitsSplitLong = 128 * kDecodeBlock;
 // (the split decoder's encoded segment words hold (j >> 5) * 4 in 13 bits:
 // qkd_decode.h encode_seg)
 constexpr int32_t kMaxChecksSplit = 65536;

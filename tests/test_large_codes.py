@@ -225,3 +225,57 @@ def test_interleaved_global_targets_equal_split(Q, monkeypatch, q, qkd_opt):
     x, y = out["1"], out["0"]
     assert torch.equal(x.iterations, y.iterations)
     assert torch.equal(x.syndromes_match, y.syndromes_match) and torch.equal(x.keys_match, y.keys_match)
+
+
+@pytest.fixture(scope="module", params=[70002, 80002])
+def long_codes(request, Q, oracle_mod, tmp_path_factory):
+    """Codes past kMaxBitsSplit (65,536 bits): N = 70,002 (M = 35,001, the
+    interleaved decoder's target syndrome words in global memory) and 80,002
+    (M = 40,001: its uncertainty words there too, decode_ilv_kernel<..., UG>);
+    N mod 64 != 0 (a ragged last key word)."""
+    n = request.param
+    m, cp, ci = regular_code(n, seed=5)
+    H = Q.HMatrix.from_check_lists(n, cp, ci)
+    cptr, cidx, bptr, bidx = H.adjacency()
+    p = str(tmp_path_factory.mktemp("long") / f"long{n}.alist")
+    write_alist(p, n, m, bptr, bidx, cptr, cidx)
+    return H, oracle_mod.Code.from_alist(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ilv,q,cap", [("1", 0.03, None), ("1", 0.07, None), ("1", 0.05, "2"), ("0", 0.04, None)])
+def test_long_code_trials_equal_oracle(Q, long_codes, oracle_mod, ilv, q, cap, qkd_opt):
+    """Long codes on the keys path: the interleaved decoder (QKD_ILV=1, two
+    workgroups so columns refill) with its uncertified frames handed to the
+    exact long-code split kernel (decode_split_kernel<..., LONG = true>; q =
+    0.07 and QKD_SPEC_CAP=2 hand many off), and the classic kernel
+    (QKD_ILV=0), against the oracle bit for bit."""
+    qkd_opt("QKD_ILV", ilv)
+    qkd_opt("QKD_ILV_GRID", "2")
+    if cap:
+        qkd_opt("QKD_SPEC_CAP", cap)
+    H, oc = long_codes
+    seeds = oracle_mod.seeds(4242, 24)
+    r = Q.run_trials(H, torch.from_numpy(seeds.view(np.int64)).cuda(), q, 0, 40)
+    torch.cuda.synchronize()
+    want = oc.trials(q, seeds, 0, 40, 100.0, True)
+    assert (r.iterations.cpu().numpy() == want["iters"]).all()
+    assert (r.syndromes_match.cpu().numpy().astype(bool) == want["sp_ok"]).all()
+    assert (r.keys_match.cpu().numpy().astype(bool) == want["key_ok"]).all()
+    assert (r.exact_qber.cpu().numpy() == want["exact_q"]).all()
+
+
+@pytest.mark.gpu
+def test_long_code_handoffs_counted(Q, long_codes, qkd_opt):
+    """QKD_SPEC_CAP=1: every frame still iterating after its first interval
+    round goes to the long-code split kernel; the replay counter counts them."""
+    qkd_opt("QKD_ILV", "1")
+    qkd_opt("QKD_SPEC_CAP", "1")
+    H, _ = long_codes
+    seeds = torch.from_numpy(Q.make_seeds(31, 256).view(np.int64)).cuda()
+    ws = Q.Workspace(H)
+    a, b, qq = Q.keygen(H, seeds, 0.03)
+    r = Q.qkd_ldpc(H, a, b, float(qq[0]), 50, workspace=ws)
+    torch.cuda.synchronize()
+    assert Q.spec_replays(ws) > 0
+    assert r.keys_match.cpu().numpy().all()
