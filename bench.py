@@ -157,12 +157,14 @@ def roofline_block(variant, alg_bytes, kernel_s, call_s, kernel_name):
     never moves the reference's two-array binary64 bytes. The headline is therefore
     the VALU issue fraction of the kernel's PMC record (separate rocprofv3 --pmc
     passes, tools/pmc_traffic.py), priced by instruction mix and reproducible from
-    that file and profiles/r*_issue_mb.txt alone:
+    that file, profiles/r*_valu_census.json and profiles/r*_issue_mb.txt alone:
         frac = sum over VALU classes (SQ_INSTS_VALU_<class> x its 4-wave issue cost)
                / (kernel cycles x 1024 SIMDs)
-    with kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs of the counted dispatches, the costs
-    measured at this decoder's occupancy (4 waves per SIMD, tools/mb/issue_mb.hip) and
-    the unclassified rest at the mean of the measured move / logic / compare costs;
+    with kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs of the counted dispatches, and a
+    class's cost the mean of its opcodes' costs measured at this decoder's occupancy
+    (4 waves per SIMD, tools/mb/issue_mb.hip), weighted by the kernel's dynamic opcode
+    census (tools/valu_census.py) -- the unclassified rest (selects, moves, shifts,
+    compares, lane reads) included;
     achieved = the needed SIMD-issue cycles per second and peak = 1024 SIMDs x the
     effective clock, so frac = achieved / peak. frac_2cyc keeps every instruction at
     2 cycles (SQ_INSTS_VALU x 2 / (kernel cycles x 1024), a lower bound of the issue
@@ -195,7 +197,14 @@ def roofline_block(variant, alg_bytes, kernel_s, call_s, kernel_name):
                 "frac": nominal, "traffic": None, "nominal": True, **base}
     pmc_s = cyc / (clk * 1e9)                        # the counted dispatches' duration
     frac_2cyc = insts * VALU_ISSUE_CYC / (cyc * N_SIMD)
-    mix = v.get("mix")
+    # the record's VALU classes priced now, from the committed opcode census and
+    # issue table (tools/pmc_traffic.py valu_mix; a record without the class
+    # counters keeps frac_2cyc)
+    mix = None
+    if "SQ_INSTS_VALU_FMA_F32" in rec.get("counters", {}):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import pmc_traffic
+        mix = pmc_traffic.valu_mix(rec["counters"], cyc)
     if mix:
         # the kernel's own VALU instruction mix priced at what 4 waves per SIMD
         # issue (tools/pmc_traffic.py valu_mix): achieved = SIMD-cycles of VALU
@@ -204,9 +213,9 @@ def roofline_block(variant, alg_bytes, kernel_s, call_s, kernel_name):
         peak = N_SIMD * clk
         out = {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G SIMD-issue-cycles/s",
                "frac": mix["frac_mix"], "frac_2cyc": frac_2cyc,
-               "formula": "frac = sum over VALU classes (PMC count x 4-wave issue cost) / (GRBM_GUI_ACTIVE/8 x "
-                          "1024 SIMDs); frac_2cyc = SQ_INSTS_VALU x 2 / (GRBM_GUI_ACTIVE/8 x 1024), every "
-                          "instruction at 2 cycles",
+               "formula": "frac = sum over VALU classes (PMC count x the census-weighted 4-wave issue cost of "
+                          "the class's opcodes) / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs); frac_2cyc = SQ_INSTS_VALU x 2 "
+                          "/ (GRBM_GUI_ACTIVE/8 x 1024), every instruction at 2 cycles",
                "mix": mix}
     else:
         out = {"bound": "valu", "achieved": insts / pmc_s / 1e9, "peak": N_SIMD / VALU_ISSUE_CYC * clk,

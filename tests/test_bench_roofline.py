@@ -19,39 +19,51 @@ def newest(pattern):
     return files[-1]
 
 
-def issue_4waves():
-    """4 waves/SIMD, ILP 8 rows of the committed issue micro-benchmark."""
-    cost = {}
-    for line in open(os.path.join(ROOT, "profiles", "r05_issue_mb.txt")):
-        f = line.split()
-        if f[2] == "4.0" and f[4] == "8":
-            cost[f[0]] = float(f[-1])
-    return cost
-
-
 def mix_priced_frac(c):
-    """Restated independently of tools/pmc_traffic.py: each VALU class of the PMC
-    record at its measured 4-wave issue cost (binary32 FMA / MUL / ADD split packed
-    vs scalar by the census shares DESIGN.md §4.3 states; the unclassified rest at
-    the mean of v_mov, v_xor, v_bfe, v_med3, v_cmp, v_cndmask with an SGPR mask),
-    over the kernel's SIMD-cycles."""
-    k = issue_4waves()
-    pk = {"FMA": (0.62, "v_pk_fma_f32", "v_fma_f32"), "MUL": (0.45, "v_pk_mul_f32", "v_mul_f32"),
-          "ADD": (0.63, "v_pk_add_f32", "v_add_f32")}
+    """Recomputed from the committed files, independently of bench.py and
+    tools/pmc_traffic.py: the dynamic opcode census (profiles/r*_valu_census.json,
+    tools/valu_census.py's classes and measured-opcode aliases) weights each
+    opcode's 4-wave issue cost (profiles/r*_issue_mb.txt) into one price per PMC
+    class; each class of the PMC record (OTHER = SQ_INSTS_VALU minus the classed
+    ones) at its price, over the kernel's SIMD-cycles."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import valu_census as V
+    census = json.load(open(newest("r*_valu_census.json")))["dynamic_per_launch"]
+    costs = V.load_costs(newest("r*_issue_mb.txt"))
+    num, den = {}, {}
+    for op, n in census.items():
+        cyc, _ = V.opcode_cost(op, costs)
+        if cyc is None:
+            continue
+        k = V.pmc_class(op)
+        num[k] = num.get(k, 0.0) + n * cyc
+        den[k] = den.get(k, 0.0) + n
+    mean = sum(num.values()) / sum(den.values())
+    price = {k: num[k] / den[k] for k in num}
     g = lambda n: c.get("SQ_INSTS_VALU_" + n, 0.0)
-    need, counted = 0.0, 0.0
-    for cls, (share, p, q) in pk.items():
-        need += g(cls + "_F32") * (share * k[p] + (1 - share) * k[q])
-        counted += g(cls + "_F32")
-    trans = (k["v_exp_f32"] + k["v_log_f32"] + k["v_rcp_f32"]) / 3
-    f64 = g("ADD_F64") + g("MUL_F64") + g("FMA_F64")
-    need += g("TRANS_F32") * trans + f64 * k["v_fma_f64"] + g("TRANS_F64") * 2 * k["v_fma_f64"]
-    need += (g("INT32") + g("CVT")) * k["v_add_u32"] + g("INT64") * 2 * k["v_add_u32"]
-    counted += g("TRANS_F32") + f64 + g("TRANS_F64") + g("INT32") + g("CVT") + g("INT64")
-    kinds = ("v_mov_b32", "v_xor_b32", "v_bfe_u32", "v_med3_f32", "v_cmp_gt_f32", "v_cndmask_b32_sgpr")
-    rest = sum(k[x] for x in kinds) / len(kinds)
-    need += max(0.0, c["SQ_INSTS_VALU"] - counted) * rest
+    cls = {"FMA_F32": g("FMA_F32"), "MUL_F32": g("MUL_F32"), "ADD_F32": g("ADD_F32"), "TRANS_F32": g("TRANS_F32"),
+           "F64": g("ADD_F64") + g("MUL_F64") + g("FMA_F64"), "TRANS_F64": g("TRANS_F64"), "INT32": g("INT32"),
+           "INT64": g("INT64"), "CVT": g("CVT")}
+    cls["OTHER"] = c["SQ_INSTS_VALU"] - sum(cls.values())
+    assert cls["OTHER"] >= 0
+    price.setdefault("TRANS_F64", 2 * costs["v_fma_f64"])
+    need = sum(n * price.get(k, mean) for k, n in cls.items())
     return need / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
+
+
+def test_census_prices_every_hot_opcode():
+    """The census's opcodes are priced by measured ones: at least 99 % of its
+    dynamic VALU count, and OTHER's price is the census-weighted mean, not a
+    fixed mean of a few opcodes."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import valu_census as V
+    census = json.load(open(newest("r*_valu_census.json")))["dynamic_per_launch"]
+    costs = V.load_costs(newest("r*_issue_mb.txt"))
+    tot = sum(census.values())
+    priced = sum(n for op, n in census.items() if V.opcode_cost(op, costs)[0] is not None)
+    assert priced / tot >= 0.99
+    other = {op: n for op, n in census.items() if V.pmc_class(op) == "OTHER"}
+    assert sum(other.values()) / tot > 0.3          # (the selects, moves and shifts the verdict asked about)
 
 
 def test_headline_roofline_is_valu_issue_from_the_pmc_record():

@@ -23,25 +23,28 @@ def test_phase_stop_patch_applies_to_the_decoder():
     assert "QKD_STOP_POINT" not in src
 
 
-def test_valu_mix_prices_the_counts_at_the_issue_table():
+def test_valu_mix_prices_the_counts_at_the_census_weighted_costs(tmp_path):
+    """A synthetic census (two OTHER opcodes, a packed and a scalar FMA) and a
+    synthetic record: each class at its census-weighted issue cost."""
+    import json
     import pmc_traffic as T
-    cost = T.issue_costs()
-    for k in ("v_fma_f32", "v_pk_fma_f32", "v_exp_f32", "v_cndmask_b32_sgpr", "v_add_u32"):
+    import valu_census as V
+    cost = V.load_costs(os.path.join(ROOT, "profiles", "r06_issue_mb.txt"))
+    for k in ("v_fma_f32", "v_pk_fma_f32", "v_exp_f32", "v_cndmask_b32_sgpr", "v_add_u32", "v_lshrrev_b32"):
         assert k in cost and cost[k] > 0
-    c = {"SQ_INSTS_VALU": 1000.0, "SQ_INSTS_VALU_FMA_F32": 100.0, "SQ_INSTS_VALU_MUL_F32": 50.0,
-         "SQ_INSTS_VALU_ADD_F32": 50.0, "SQ_INSTS_VALU_TRANS_F32": 20.0, "SQ_INSTS_VALU_INT32": 80.0,
-         "SQ_INSTS_VALU_INT64": 10.0}
+    census = {"v_cndmask_b32": 30.0, "v_lshrrev_b32": 10.0, "v_pk_fma_f32": 3.0, "v_fma_f32": 1.0,
+              "v_add_u32": 5.0, "v_exp_f32": 2.0}
+    p = tmp_path / "census.json"
+    p.write_text(json.dumps({"dynamic_per_launch": census}))
+    c = {"SQ_INSTS_VALU": 1000.0, "SQ_INSTS_VALU_FMA_F32": 100.0, "SQ_INSTS_VALU_TRANS_F32": 20.0,
+         "SQ_INSTS_VALU_INT32": 80.0}
     cycles = 100.0                                     # per XCD-averaged GPU cycle count
-    m = T.valu_mix(c, cycles)
-    s = T.PACKED_SHARE
-    want = (100 * (s["FMA_F32"] * cost["v_pk_fma_f32"] + (1 - s["FMA_F32"]) * cost["v_fma_f32"])
-            + 50 * (s["MUL_F32"] * cost["v_pk_mul_f32"] + (1 - s["MUL_F32"]) * cost["v_mul_f32"])
-            + 50 * (s["ADD_F32"] * cost["v_pk_add_f32"] + (1 - s["ADD_F32"]) * cost["v_add_f32"])
-            + 20 * (cost["v_exp_f32"] + cost["v_log_f32"] + cost["v_rcp_f32"]) / 3
-            + 80 * cost["v_add_u32"] + 10 * 2 * cost["v_add_u32"]
-            + (1000 - 310) * sum(cost[k] for k in T.OTHER_KINDS) / len(T.OTHER_KINDS))
+    m = T.valu_mix(c, cycles, census_path=str(p), issue_path=os.path.join(ROOT, "profiles", "r06_issue_mb.txt"))
+    other = (30 * cost["v_cndmask_b32_sgpr"] + 10 * cost["v_lshrrev_b32"]) / 40
+    fma = (3 * cost["v_pk_fma_f32"] + 1 * cost["v_fma_f32"]) / 4
+    want = 100 * fma + 20 * cost["v_exp_f32"] + 80 * cost["v_add_u32"] + (1000 - 200) * other
     assert m["simd_cycles_needed"] == pytest.approx(want, rel=1e-12)
     assert m["frac_mix"] == pytest.approx(want / (cycles * 1024), rel=1e-12)
-    assert m["counts"]["OTHER"] == 690.0
-    # a record without the class counters has no mix
-    assert T.valu_mix({"SQ_INSTS_VALU": 1.0}, cycles) is None
+    assert m["counts"]["OTHER"] == 800.0
+    # a record without the VALU total has no mix
+    assert T.valu_mix({"SQ_X": 1.0}, cycles) is None

@@ -18,7 +18,11 @@ __global__ __launch_bounds__(1024) void k(float* out, unsigned long long* cyc, i
         y[u] = f2{x[u], x[u] + 0.25f};
         d[u] = (double)x[u];
     }
+    unsigned long long sm[ILP];
+    int si[ILP];
+    for (int u = 0; u < ILP; ++u) { sm[u] = 0; si[u] = 0; }
     const unsigned long long msk = __builtin_amdgcn_readfirstlane((int)(a > 0.0f)) ? 0x5555555555555555ull : 0ull;
+    if constexpr (OP == 44) asm volatile("s_mov_b64 vcc, %0" : : "s"(msk) : "vcc");
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int i = 0; i < iters; ++i) {
@@ -48,12 +52,49 @@ __global__ __launch_bounds__(1024) void k(float* out, unsigned long long* cyc, i
             // (the select's mask in an SGPR pair, as the compiler emits it; OP 11
             // reads VCC, which the loop's own compare may be writing)
             if constexpr (OP == 19) asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x[u]) : "v"(a), "s"(msk));
+            // round 6: the rest of the decoder's dynamic VALU census (tools/valu_census.py)
+            if constexpr (OP == 20) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(x[u]));
+            if constexpr (OP == 21) asm volatile("v_and_b32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 22) asm volatile("v_or_b32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 23) asm volatile("v_max_f32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 24) asm volatile("v_min_f32 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 25) asm volatile("v_cmp_ne_u32 %0, %1, %2" : "=s"(sm[u]) : "v"(x[u]), "v"(a));
+            if constexpr (OP == 26) asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(si[u]) : "v"(x[u]));
+            if constexpr (OP == 27) asm volatile("v_readlane_b32 %0, %1, 5" : "=s"(si[u]) : "v"(x[u]));
+            if constexpr (OP == 28) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 29) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(x[u]));
+            if constexpr (OP == 30) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(d[u]));
+            if constexpr (OP == 31) asm volatile("v_bcnt_u32_b32 %0, %0, 0" : "+v"(x[u]));
+            if constexpr (OP == 32) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(x[u]) : "v"(a), "v"(b));
+            if constexpr (OP == 33) asm volatile("v_pk_mov_b32 %0, %1, %0 op_sel:[1,0]" : "+v"(d[u]) : "v"(d[0]));
+            if constexpr (OP == 34) asm volatile("v_cmp_lt_f64 %0, %1, %2" : "=s"(sm[u]) : "v"(d[u]), "v"(d[0]));
+            if constexpr (OP == 35) asm volatile("v_add_u16 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 36) asm volatile("v_bfi_b32 %0, %1, %2, %0" : "+v"(x[u]) : "v"(a), "v"(b));
+            if constexpr (OP == 37) asm volatile("v_fmamk_f32 %0, %0, 0x3f800000, %1" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 38) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(x[u]) : "v"(d[u]));
+            if constexpr (OP == 39) asm volatile("v_cndmask_b32 %0, %0, -%1, %2" : "+v"(x[u]) : "v"(a), "s"(msk));
+            if constexpr (OP == 40) asm volatile("v_mul_lo_u16 %0, %1, %0" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 41) asm volatile("v_lshrrev_b32_sdwa %0, 3, %0 dst_sel:DWORD src1_sel:WORD_1" : "+v"(x[u]));
+            if constexpr (OP == 42) asm volatile("v_add_f64 %0, %1, %0" : "+v"(d[u]) : "v"(d[0]));
+            // the VCC select again, VCC written first (OP 44) and in the VOP3 encoding (OP 43)
+            if constexpr (OP == 43) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(x[u]) : "v"(a));
+            if constexpr (OP == 44) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[u]) : "v"(a));
+            // a select among other work: one select per three FMAs (VOP2 / VOP3 select)
+            if constexpr (OP == 45)
+                asm volatile("v_fma_f32 %0, %2, %3, %0\n\tv_fma_f32 %0, %2, %3, %0\n\tv_fma_f32 %0, %2, %3, %0\n\t"
+                             "v_cndmask_b32 %1, %1, %2, vcc" : "+v"(x[u]), "+v"(y[u].x) : "v"(a), "v"(b));
+            if constexpr (OP == 46)
+                asm volatile("v_fma_f32 %0, %2, %3, %0\n\tv_fma_f32 %0, %2, %3, %0\n\tv_fma_f32 %0, %2, %3, %0\n\t"
+                             "v_cndmask_b32_e64 %1, %1, %2, vcc" : "+v"(x[u]), "+v"(y[u].x) : "v"(a), "v"(b));
+            if constexpr (OP == 47)
+                asm volatile("v_fma_f32 %0, %2, %3, %0\n\tv_fma_f32 %0, %2, %3, %0\n\tv_fma_f32 %0, %2, %3, %0\n\t"
+                             "v_fma_f32 %1, %2, %3, %1" : "+v"(x[u]), "+v"(y[u].x) : "v"(a), "v"(b));
         }
     }
     __syncthreads();
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     float s = 0;
-    for (int u = 0; u < ILP; ++u) s += x[u] + y[u].x + y[u].y + (float)d[u];
+    for (int u = 0; u < ILP; ++u) s += x[u] + y[u].x + y[u].y + (float)d[u] + (float)(sm[u] & 1u) + (float)(si[u] & 1);
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
@@ -108,6 +149,37 @@ int main() {
         run<17, 8>("v_cmp_gt_f32", d, dc, cus, c[0], c[1]);
         run<18, 8>("v_xor_b32", d, dc, cus, c[0], c[1]);
         run<19, 8>("v_cndmask_b32_sgpr", d, dc, cus, c[0], c[1]);
+        if (c[0] != 1024 || c[1] != 1) continue;      // (the rest at the decoder's 4 waves/SIMD only)
+        run<20, 8>("v_lshrrev_b32", d, dc, cus, c[0], c[1]);
+        run<21, 8>("v_and_b32", d, dc, cus, c[0], c[1]);
+        run<22, 8>("v_or_b32", d, dc, cus, c[0], c[1]);
+        run<23, 8>("v_max_f32", d, dc, cus, c[0], c[1]);
+        run<24, 8>("v_min_f32", d, dc, cus, c[0], c[1]);
+        run<25, 8>("v_cmp_ne_u32", d, dc, cus, c[0], c[1]);
+        run<26, 8>("v_readfirstlane_b32", d, dc, cus, c[0], c[1]);
+        run<27, 8>("v_readlane_b32", d, dc, cus, c[0], c[1]);
+        run<28, 8>("v_lshl_add_u32", d, dc, cus, c[0], c[1]);
+        run<29, 8>("v_lshlrev_b32", d, dc, cus, c[0], c[1]);
+        run<30, 8>("v_lshrrev_b64", d, dc, cus, c[0], c[1]);
+        run<31, 8>("v_bcnt_u32_b32", d, dc, cus, c[0], c[1]);
+        run<32, 8>("v_mad_u32_u24", d, dc, cus, c[0], c[1]);
+        run<33, 8>("v_pk_mov_b32", d, dc, cus, c[0], c[1]);
+        run<34, 8>("v_cmp_lt_f64", d, dc, cus, c[0], c[1]);
+        run<35, 8>("v_add_u16", d, dc, cus, c[0], c[1]);
+        run<36, 8>("v_bfi_b32", d, dc, cus, c[0], c[1]);
+        run<37, 8>("v_fmamk_f32", d, dc, cus, c[0], c[1]);
+        run<38, 8>("v_cvt_f32_f64", d, dc, cus, c[0], c[1]);
+        run<39, 8>("v_cndmask_b32_neg", d, dc, cus, c[0], c[1]);
+        run<40, 8>("v_mul_lo_u16", d, dc, cus, c[0], c[1]);
+        run<41, 8>("v_lshrrev_b32_sdwa", d, dc, cus, c[0], c[1]);
+        run<42, 8>("v_add_f64", d, dc, cus, c[0], c[1]);
+        run<43, 8>("v_cndmask_b32_vcc_e64", d, dc, cus, c[0], c[1]);
+        run<44, 8>("v_cndmask_b32_vcc_set", d, dc, cus, c[0], c[1]);
+        run<11, 1>("v_cndmask_b32", d, dc, cus, c[0], c[1]);
+        run<45, 8>("3fma+cndmask_e32", d, dc, cus, c[0], c[1]);     // (cycles per 4 instructions)
+        run<46, 8>("3fma+cndmask_e64", d, dc, cus, c[0], c[1]);
+        run<47, 8>("4fma", d, dc, cus, c[0], c[1]);
+        run<19, 1>("v_cndmask_b32_sgpr", d, dc, cus, c[0], c[1]);
     }
     return 0;
 }

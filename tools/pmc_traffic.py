@@ -36,63 +36,70 @@ def collect(dirs):
 
 # VALU issue cost per wave64 instruction per SIMD at 4 waves per SIMD (the split
 # decoder's occupancy), ILP 8, shader cycles: tools/mb/issue_mb.hip,
-# profiles/r05_issue_mb.txt. Packed binary32 ops count ONCE in the
-# SQ_INSTS_VALU_{FMA,MUL,ADD}_F32 counters (the ISA census of the check-phase
-# loops times their trip counts reproduces FMA_F32 to 2 %), so each class is
-# priced at its packed share (same census) of the packed cost.
-ISSUE_MB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                        "profiles", "r05_issue_mb.txt")
+# profiles/r06_issue_mb.txt (one row per opcode the decoder issues). Each PMC
+# class (SQ_INSTS_VALU_<class>; OTHER = the rest of SQ_INSTS_VALU) is priced at
+# the mean cost of ITS opcodes weighted by the decoder's dynamic opcode census
+# (tools/valu_census.py: the kernel's ISA split into phases, each phase's
+# innermost-loop mix scaled to the per-phase PMC VALU count; committed as
+# profiles/r*_valu_census.json). So packed and scalar binary32 FMAs, and the
+# selects, moves, shifts, compares and lane reads of OTHER, each count at their
+# own measured cost in the proportion the kernel executes them.
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import valu_census  # noqa: E402
+
+PROFILES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
+PMC_CLASSES = ("FMA_F32", "MUL_F32", "ADD_F32", "TRANS_F32", "F64", "TRANS_F64", "INT32", "INT64", "CVT")
 
 
-def issue_costs(path=ISSUE_MB, waves=4.0, ilp=8):
-    """{instruction: cycles per wave-instruction per SIMD} at `waves` waves/SIMD and
-    the given ILP, from the committed issue micro-benchmark output."""
-    out = {}
-    for line in open(path):
-        f = line.split()
-        if len(f) == 7 and float(f[2]) == waves and int(f[4]) == ilp:
-            out[f[0]] = float(f[6])
-    return out
+def newest(pattern):
+    import glob
+    fs = sorted(glob.glob(os.path.join(PROFILES, pattern)))
+    return fs[-1] if fs else None
 
 
-# packed shares per class (census of the paired and iteration-2 check-phase steps
-# and the speculative bit-phase rounds, weighted by their config-2 trip counts)
-PACKED_SHARE = {"FMA_F32": 0.62, "MUL_F32": 0.45, "ADD_F32": 0.63}
-OTHER_KINDS = ("v_mov_b32", "v_xor_b32", "v_bfe_u32", "v_med3_f32", "v_cmp_gt_f32", "v_cndmask_b32_sgpr")
-
-
-def valu_mix(c, cycles):
-    """The VALU instruction mix of the PMC record priced at the 4-wave issue
-    costs: the SIMD-cycles the kernel's VALU stream needs at those rates, and the
-    share of the kernel's SIMD-cycles that is (frac_mix = the issue-bound
-    fraction at the kernel's own instruction mix)."""
-    keys = ["SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_ADD_F32",
-            "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_INT32"]
-    if not all(k in c for k in keys + ["SQ_INSTS_VALU"]) or not cycles:
-        return None
-    I = issue_costs()
-    price = {
-        "FMA_F32": PACKED_SHARE["FMA_F32"] * I["v_pk_fma_f32"] + (1 - PACKED_SHARE["FMA_F32"]) * I["v_fma_f32"],
-        "MUL_F32": PACKED_SHARE["MUL_F32"] * I["v_pk_mul_f32"] + (1 - PACKED_SHARE["MUL_F32"]) * I["v_mul_f32"],
-        "ADD_F32": PACKED_SHARE["ADD_F32"] * I["v_pk_add_f32"] + (1 - PACKED_SHARE["ADD_F32"]) * I["v_add_f32"],
-        "TRANS_F32": (I["v_exp_f32"] + I["v_log_f32"] + I["v_rcp_f32"]) / 3,
-        "F64": I["v_fma_f64"], "TRANS_F64": 2 * I["v_fma_f64"],
-        "INT32": I["v_add_u32"], "INT64": 2 * I["v_add_u32"], "CVT": I["v_add_u32"],
-        # the rest (selects, compares, moves, logic, med3 / max, lane reads): the
-        # mean of the measured v_mov, v_xor, v_bfe, v_med3, v_cmp and v_cndmask
-        # (SGPR mask, as compiled) costs
-        "OTHER": sum(I[k] for k in OTHER_KINDS) / len(OTHER_KINDS),
-    }
+def pmc_class_counts(c):
+    """The PMC record's VALU instructions per class; OTHER = the unclassified rest."""
     g = lambda k: c.get("SQ_INSTS_VALU_" + k, 0.0)
     n = {"FMA_F32": g("FMA_F32"), "MUL_F32": g("MUL_F32"), "ADD_F32": g("ADD_F32"), "TRANS_F32": g("TRANS_F32"),
          "F64": g("ADD_F64") + g("MUL_F64") + g("FMA_F64"), "TRANS_F64": g("TRANS_F64"),
          "INT32": g("INT32"), "INT64": g("INT64"), "CVT": g("CVT")}
     n["OTHER"] = max(0.0, c["SQ_INSTS_VALU"] - sum(n.values()))
+    return n
+
+
+def census_prices(census_path=None, issue_path=None):
+    """{class: cycles} from the committed census and issue table; a class the
+    census does not see (or with no measured opcode) takes the FMA_F32 price
+    for F64 work's 2x and the census-wide mean otherwise."""
+    census_path = census_path or newest("r*_valu_census.json")
+    issue_path = issue_path or newest("r*_issue_mb.txt")
+    rec = json.load(open(census_path))
+    costs = valu_census.load_costs(issue_path)
+    cp = valu_census.class_prices(rec["dynamic_per_launch"], costs)
+    tot = sum(v["count"] for v in cp.values() if v["cycles"])
+    mean = sum(v["count"] * v["cycles"] for v in cp.values() if v["cycles"]) / tot
+    price = {k: (cp[k]["cycles"] if k in cp and cp[k]["cycles"] else mean) for k in PMC_CLASSES + ("OTHER",)}
+    if not (cp.get("TRANS_F64") or {}).get("cycles"):
+        price["TRANS_F64"] = 2 * costs.get("v_fma_f64", mean)
+    return price, cp, os.path.basename(census_path), os.path.basename(issue_path)
+
+
+def valu_mix(c, cycles, census_path=None, issue_path=None):
+    """The PMC record's VALU classes priced at their census-weighted 4-wave issue
+    costs: the SIMD-cycles the kernel's VALU stream needs, and the share of the
+    kernel's SIMD-cycles that is (frac_mix, the issue-bound fraction at the
+    kernel's own instruction mix)."""
+    if "SQ_INSTS_VALU" not in c or not cycles:
+        return None
+    price, cp, csrc, isrc = census_prices(census_path, issue_path)
+    n = pmc_class_counts(c)
     need = sum(n[k] * price[k] for k in n)
-    return {"counts": n, "price_cycles_4waves": price, "packed_share": PACKED_SHARE,
-            "issue_source": "tools/mb/issue_mb.hip at 4 waves/SIMD, ILP 8 (profiles/r05_issue_mb.txt)",
+    return {"counts": n, "price_cycles_4waves": price,
+            "census": {k: {"count": v["count"], "measured_share": v["measured_share"]} for k, v in cp.items()},
+            "census_source": "profiles/" + csrc, "issue_source": "profiles/" + isrc,
             "simd_cycles_needed": need, "frac_mix": need / (cycles * N_SIMD),
-            "formula": "frac_mix = sum_class(count x price) / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)"}
+            "formula": "frac_mix = sum_class(PMC count x census-weighted 4-wave cost of the class's opcodes) / "
+                       "(GRBM_GUI_ACTIVE/8 x 1024 SIMDs)"}
 
 
 def main():
