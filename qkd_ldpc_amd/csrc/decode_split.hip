@@ -62,7 +62,7 @@ struct SegWeights {
         if constexpr (DC <= 8) {
             // (idle lanes: a degree-1 segment starting at lane 0, p = lane;
             // any p >= 1 gives their only weight, entry 0)
-            w = wtab + ((deg - 1) * DC + min(p, DC - 1)) * DC;
+            w = wtab + (deg * 8 + min(p, DC - 1)) * DC;
             mask = 0;
         } else {
             // 64-bit: deg reaches 64 in the widest bucket and p (= lane - start)
@@ -83,6 +83,7 @@ __device__ __forceinline__ int seg_start(uint2 w) { return (int)((w.y >> kSegSta
 __device__ __forceinline__ uint32_t seg_wi(uint2 w) { return (w.y >> kSegWiShift) & 255u; }
 template <int DC>
 __device__ __forceinline__ int seg_deg(uint2 w) {
+    if constexpr (DC <= 8) return (int)((w.y >> (kSegWiShift + 3)) & 15u);
     return DC <= 16 ? (int)(seg_wi(w) / (uint32_t)DC) + 1 : (int)seg_wi(w) + 1;
 }
 template <int DC>
@@ -638,8 +639,12 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         const f2 bv = qkds::unpack_iv(xv);
         neg = bv.x < 0.0f;
         const bool ok = bv.x == bv.x;
-        bad |= __ballot(!ok && pw_slot(w) != dummy);
-        return ok ? neg_iv_if(neg, bv) : f2{0.0f, 0.0f};
+        // (an uncertain entry stays NaN in the row: the round aborts on it, so
+        // what it does to the other lanes' sums never stands; the dummy
+        // column's entry is finite. Two ballots of plain compares: a ballot of
+        // their conjunction materialises it as 0 / 1 and compares it back)
+        bad |= __ballot(!ok) & __ballot(pw_slot(w) != dummy);
+        return neg_iv_if(neg, bv);
     };
     uint2 wt = plan_word(prs, t, lane);
     uint2 wn = plan_word(prs, t + NW, lane);
@@ -730,7 +735,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         // |.|lo > 1e-30, of which the second alone decides: |.|lo is -hi
         // when neg, lo otherwise; NaN fails either way)
         const bool ok = ab.x > 1.0e-30f;
-        bad |= __ballot(!ok && pw_slot(w) != dummy);
+        bad |= __ballot(!ok) & __ballot(pw_slot(w) != dummy);
         return ok;
     };
     // (the plan has kPlanPadTasks idle tasks past n_tasks: loads ahead need no test)
@@ -761,7 +766,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         const uint32_t sb_n = seg_sbit(w_n);
         bool neg_n;
         f2 ab_n;
-        const bool ok_n = input(ms.pick(x_n), w_n, neg_n, ab_n);
+        input(ms.pick(x_n), w_n, neg_n, ab_n);
         // this task's extrinsic sums (as spec_check_phase_psi)
         wave_lds_sync();
         const int start = seg_start(w_t);
@@ -779,8 +784,11 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
         const uint32_t sigma = sb_t ^ seg_parity_enc<DC>(sgn_t, w_t) ^ (neg_t ? 1u : 0u);
         ms.st_w(slot(w_t), qkds::pack_iv(neg_iv_if(sigma != 0u, m)));
-        // the next task's input bounds into the row
-        row[lane] = qkds::pack_iv(ok_n ? ph_n : f2{0.0f, 0.0f});
+        // the next task's input bounds into the row: an uncertified entry as
+        // phi_pair left it -- finite for the dummy column's 0 (phi_pair
+        // evaluates at no less than kPhiTiny), anything for the others, whose
+        // round aborts (no select: -3 VALU per task with the ballots above)
+        row[lane] = qkds::pack_iv(ph_n);
         sgn_t = __ballot(neg_n);
         neg_t = neg_n;
         sb_t = sb_n;
@@ -1167,7 +1175,8 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
     float* wtab = reinterpret_cast<float*>(smem + L.wtab);
     // (min-sum: the additive masks of ms_split_check_phase, 0 / +inf)
     for (int e = threadIdx.x; e < seg_weight_entries(DC); e += kDecodeBlock) {
-        const int k = e % DC, p = (e / DC) % DC, deg = e / (DC * DC) + 1;
+        const int k = e % DC;
+        const int p = (e / DC) % 8, deg = e / (DC * 8);      // (rows deg * 8 + p, encode_seg)
         const bool in = k < deg && k != p;
         wtab[e] = MSR ? (in ? 0.0f : __builtin_inff()) : (in ? 1.0f : 0.0f);
     }

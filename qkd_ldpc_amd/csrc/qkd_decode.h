@@ -576,7 +576,12 @@ __device__ void second_table_fill(const DeviceCode& c, const double* ctab, doubl
 // segment of degree deg sums row entry k with weight (k < deg && k != p).
 // Buckets up to 8 read them from an LDS table (wtab[deg - 1][p][k], two
 // per ds_read_b64) instead of extracting and converting mask bits per entry.
-__host__ __device__ inline int seg_weight_entries(int dc) { return dc <= 8 ? dc * dc * dc : 0; }
+// Buckets DC <= 8 index their segment-weight rows by deg * 8 + p (encode_seg),
+// so a lane's degree is one bit-field read of its plan word instead of a
+// division by DC (rows of degree 0 and p >= DC unused; -3 VALU per check-phase
+// task; with the check phases' select-free row entries -3.4 % per config-2
+// batch, profiles/r06_ab.txt)
+__host__ __device__ inline int seg_weight_entries(int dc) { return dc <= 8 ? 9 * 8 * dc : 0; }
 
 struct SplitLds {
     size_t tsyn, xsyn, qsyn, xunc, zw, aw, tval, ctab, tab2, ftab, ctl, wtab, msg, bytes;
@@ -630,14 +635,16 @@ __host__ __device__ inline uint32_t encode_slot(uint32_t x, uint32_t S, uint32_t
 //   bits 0-4    j & 31: the target bit's position in its syndrome word (a
 //               shift by the whole word uses these bits only)
 //   bits 5-10   start: the segment's first lane
-//   bits 11-18  wi: DC <= 16: (deg - 1) * DC + min(lane - start, DC - 1), the
-//               row of the segment-weight table (SegWeights); wider buckets: deg - 1
+//   bits 11-18  wi: the row of the segment-weight table (SegWeights): DC <= 8:
+//               deg * 8 + min(lane - start, DC - 1); DC = 16: (deg - 1) * DC +
+//               min(lane - start, DC - 1); wider buckets: deg - 1
 //   bits 19-31  (j >> 5) * 4: the byte offset of the check's syndrome word
 // (needs M <= 65536: the split decoder's limit).
 constexpr uint32_t kSegStartShift = 5, kSegWiShift = 11, kSegWordShift = 19;
 __host__ __device__ inline uint32_t encode_seg(uint32_t j, uint32_t start, uint32_t deg, uint32_t lane, uint32_t dc) {
     const uint32_t p = lane - start;
-    const uint32_t wi = dc <= 16 ? (deg - 1) * dc + (p < dc - 1 ? p : dc - 1) : deg - 1;
+    const uint32_t pc = p < dc - 1 ? p : dc - 1;
+    const uint32_t wi = dc <= 8 ? deg * 8 + pc : dc <= 16 ? (deg - 1) * dc + pc : deg - 1;
     return (j & 31u) | (start << kSegStartShift) | (wi << kSegWiShift) | (((j >> 5) * 4u) << kSegWordShift);
 }
 

@@ -48,6 +48,9 @@ constexpr float kLn2 = 0.693147180559945f;
 constexpr float kInvLn2 = 1.44269504088896f;
 constexpr float kRefSumAbs = 4.0e-14f;     // reference roundings (2.8e-14 in the phi domain), psi units
 constexpr float kPhiHuge = 80.0f;          // phi evaluated at most here (e^-80: a normal binary32)
+// phi_pair evaluates its input bound at no less than this: the check phase
+// certifies only |b2c| > 1e-30, so the bounds of smaller inputs are never used
+constexpr float kPhiTiny = 1.0e-30f;
 constexpr float kPsiHuge = 115.0f;         // the same bound for psi-unit sums (115 ln 2 < 80)
 constexpr float kPsiSumMax = 865.0f;       // 600 / ln 2: the reference's product would underflow
 
@@ -209,7 +212,9 @@ __device__ __forceinline__ PhiVal2 phi_core_pair(f2 x, f2 u, f2 lg) {
 __device__ __forceinline__ void phi_pair(float a, float b, float s_lo, float s_hi, f2& in, f2& out) {
     // evaluation points: phi_bounds at a1 = min(a, kPhiHuge); phi_bounds_out
     // at P = min(s_lo, kPsiHuge) (s_hi when the sum reached zero), x = P ln 2
-    const float a1 = __builtin_amdgcn_fmed3f(a, 0.0f, kPhiHuge);
+    // (at no less than kPhiTiny: an input the check phase does not certify,
+    // a <= 1e-30, still gives finite bounds -- the dummy column's 0)
+    const float a1 = __builtin_amdgcn_fmed3f(a, kPhiTiny, kPhiHuge);
     const bool zero = !(s_lo > 0.0f);
     const float P = __builtin_fminf(zero ? s_hi : s_lo, kPsiHuge);
     // u = e^-x: half 0 by exp_neg's argument split, half 1 = 2^-P
