@@ -104,6 +104,17 @@ __device__ __forceinline__ uint32_t seg_sbit(uint2 w) {
     return (word >> (w.y & 31u)) & 1u;
 }
 // parity of the segment's bits in a wave ballot (seg_parity of qkd_decode.h)
+// xor the low bits of add (two one-bit terms at most): the popcount's own
+// accumulator (v_bcnt_u32_b32) takes the sum, no separate xors (-0.7 % per
+// config-2 batch, profiles/r06_ab.txt)
+template <int DC>
+__device__ __forceinline__ uint32_t seg_parity_acc(uint64_t ballot, uint2 w, uint32_t add) {
+    const uint64_t sh = ballot >> seg_start(w);
+    const uint32_t deg = (uint32_t)seg_deg<DC>(w);
+    if constexpr (DC < 32) return ((uint32_t)__popc(__builtin_amdgcn_ubfe((uint32_t)sh, 0, deg)) + add) & 1u;
+    const uint64_t m = deg >= 64 ? ~0ull : ((1ull << deg) - 1ull);
+    return ((uint32_t)__popcll(sh & m) + add) & 1u;
+}
 template <int DC>
 __device__ __forceinline__ uint32_t seg_parity_enc(uint64_t ballot, uint2 w) {
     const uint64_t sh = ballot >> seg_start(w);
@@ -682,7 +693,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         // canonicalisation fminf needs for a kernel argument)
         m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
         m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
-        const uint32_t sigma = sb_t ^ seg_parity_enc<DC>(sgn_t, w_t) ^ (neg_t ? 1u : 0u);
+        const uint32_t sigma = seg_parity_acc<DC>(sgn_t, w_t, sb_t + (neg_t ? 1u : 0u));
         ms.st_w(slot(w_t), qkds::pack_iv(neg_iv_if(sigma != 0u, m)));
         row[lane] = qkds::pack_iv(ph_n);
         sgn_t = __ballot(neg_n);
@@ -782,7 +793,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         // this task's c2b: threshold_matrix (:246-249) on the magnitude, the sign
         m.x = __builtin_amdgcn_fmed3f(m.x, 0.0f, thr_dn);
         m.y = __builtin_amdgcn_fmed3f(m.y, 0.0f, thr_up);
-        const uint32_t sigma = sb_t ^ seg_parity_enc<DC>(sgn_t, w_t) ^ (neg_t ? 1u : 0u);
+        const uint32_t sigma = seg_parity_acc<DC>(sgn_t, w_t, sb_t + (neg_t ? 1u : 0u));
         ms.st_w(slot(w_t), qkds::pack_iv(neg_iv_if(sigma != 0u, m)));
         // the next task's input bounds into the row: an uncertified entry as
         // phi_pair left it -- finite for the dummy column's 0 (phi_pair
@@ -1320,6 +1331,9 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             xunc[w] = 0;
         }
         __syncthreads();
+#ifdef QKD_PRO_MARKS
+        pc.mark(5);      // (diagnostic: the loop top's clear and barrier as phase 5)
+#endif
         const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl[1]);   // (uniform to the compiler)
         if (f >= a.n_frames) break;
         if (tid == 0) next_f = claim();
@@ -1348,6 +1362,9 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 qsyn[q] = sy[m_words + q];
             }
             __syncthreads();
+#ifdef QKD_PRO_MARKS
+            pc.mark(6);  // (diagnostic: the frame's loads and their barrier as phase 6)
+#endif
         }
         // Bob's bits of this thread's bit-phase rounds (round r: internal bit
         // i = tid + r * kDecodeBlock; N <= 64 * kDecodeBlock, kMaxBitsSplit).
@@ -1490,7 +1507,11 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                                                                    wave, lane);
                 __syncthreads();
             }
+#ifdef QKD_PRO_MARKS
+            pc.mark(1);
+#else
             pc.mark((FOLDS && it < 2 && fold1) ? 5 + (int)it : 1);
+#endif
             // the b2c of this bit phase are read only by a next iteration
             const bool keep = it + 1 < a.max_it;
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
