@@ -204,7 +204,9 @@ def roofline_block(variant, alg_bytes, kernel_s, call_s, kernel_name):
     if "SQ_INSTS_VALU_FMA_F32" in rec.get("counters", {}):
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import pmc_traffic
-        mix = pmc_traffic.valu_mix(rec["counters"], cyc)
+        # (a binary32 variant: its own kernel's census, tools/valu_census.py variant)
+        cpath = None if variant == "sp_f64" else pmc_traffic.newest(f"r*_valu_census_{variant}.json")
+        mix = pmc_traffic.valu_mix(rec["counters"], cyc, census_path=cpath)
     if mix:
         # the kernel's own VALU instruction mix priced at what 4 waves per SIMD
         # issue (tools/pmc_traffic.py valu_mix): achieved = SIMD-cycles of VALU

@@ -5,9 +5,10 @@ input) is split into the decoder's phases by source line: every instruction
 belongs to the phase of the last decode_split.hip line the .loc directives named
 before it (helpers inlined from other files, and decode_split.hip's own small
 helpers above the phase functions, inherit that context). Inside each phase the
-instructions of its innermost loops stand for its dynamic mix (the loop bodies
-execute once per task / bit batch; the straight-line code around them once per
-phase). Each phase's mix is then scaled to the VALU count the per-phase PMC
+instructions of its innermost hot loops (at least MIN_LOOP_VALU VALU
+instructions: a task or a bit round) stand for its dynamic mix (the loop
+bodies execute once per task / bit batch; the straight-line code around them
+once per phase). Each phase's mix is then scaled to the VALU count the per-phase PMC
 record measured for it (tools/phase_pmc.py: phase-stop builds, counters of stop
 K minus stop K - 1), which gives dynamic counts per opcode.
 
@@ -17,6 +18,7 @@ issue costs tools/mb/issue_mb.hip measures per opcode (profiles/r06_issue_mb.txt
 
     python tools/valu_census.py census KERNEL.s PHASE_PMC.json OUT.json
     (tools/census_isa.sh OUT.s PHASE_PMC.json OUT.json builds KERNEL.s first)
+    python tools/valu_census.py variant KERNEL.s VARIANT W_CHECK W_BIT OUT.json
 
 Round 6 (profiles/r06_valu_census.json, from profiles/r06_phase_pmc.json): of
 592M VALU per config-2 launch 306M are OTHER, led by v_cndmask_b32 (82M: the
@@ -131,13 +133,22 @@ def parse(path, pat, table):
     return ins, loops
 
 
-def innermost(loops):
-    """Loops that contain no other loop."""
+def innermost(loops, ins=None, min_valu=0):
+    """Loops that contain no other loop. With ins and min_valu: among the loops
+    of at least min_valu VALU instructions only (a phase's batch loop counts as
+    innermost around the few-instruction loops the compiler leaves inside it --
+    exec-mask waterfalls, zero fills -- which themselves are dropped)."""
+    if ins is not None and min_valu:
+        loops = [(a, b) for a, b in loops if sum(1 for o, _ in ins[a:b + 1] if o.startswith("v_")) >= min_valu]
     out = []
     for a, b in loops:
         if not any((c, d) != (a, b) and a <= c and d <= b for c, d in loops):
             out.append((a, b))
     return out
+
+
+# a hot loop has at least this many VALU instructions (one task or bit round)
+MIN_LOOP_VALU = 40
 
 
 # SQ_INSTS_VALU_* class of an opcode: the PMC's own classes (packed binary32
@@ -271,7 +282,7 @@ def census(s_path, phase_json, out_path, src_path=None):
     src_path = src_path or os.path.join(ROOT, "qkd_ldpc_amd", "csrc", SRC)
     table = regions(src_path)
     ins, loops = parse(s_path, KERNEL, table)
-    inner = innermost(loops)
+    inner = innermost(loops, ins, MIN_LOOP_VALU)
     # per region: static counts of the innermost-loop instructions (hot) and of all
     hot = collections.defaultdict(collections.Counter)
     allc = collections.defaultdict(collections.Counter)
@@ -327,7 +338,47 @@ def census(s_path, phase_json, out_path, src_path=None):
     return rec
 
 
+# The binary32 variants (no per-phase PMC record): their kernels' check- and
+# bit-phase innermost-loop mixes weighted by the phases' shader-clock shares
+# (bench.py --phase-timing, profiles/r06_variants.txt) -- a coarser census
+VARIANTS = {
+    "sp_f32": ("decode_split_kernelILi1ELi1ELi6ELb1ELi0ELb0E", ("sp32_check",), ("sp32_bit",)),
+    "minsum": ("decode_split_kernelILi1ELi5ELi6ELb1ELi0ELb0E", ("ms_check",), ("sp32_bit",)),
+    "minsum_sc": ("decode_split_kernelILi1ELi6ELi6ELb1ELi0ELb0E", ("ms_check",), ("sp32_bit",)),
+}
+
+
+def census_variant(s_path, variant, w_check, w_bit, out_path, src_path=None):
+    src_path = src_path or os.path.join(ROOT, "qkd_ldpc_amd", "csrc", SRC)
+    sym, creg, breg = VARIANTS[variant]
+    table = regions(src_path)
+    ins, loops = parse(s_path, sym, table)
+    in_loop = [False] * len(ins)
+    for a, b in innermost(loops, ins, MIN_LOOP_VALU):
+        for i in range(a, b + 1):
+            in_loop[i] = True
+    mix = {}
+    for regs, w in ((creg, w_check), (breg, w_bit)):
+        c = collections.Counter(o for i, (o, r) in enumerate(ins) if in_loop[i] and r in regs and o.startswith("v_"))
+        tot = sum(c.values())
+        for o, n in c.items():
+            mix[o] = mix.get(o, 0.0) + w * n / tot
+    rec = {"kernel": sym, "variant": variant, "s_file": os.path.basename(s_path),
+           "weights": {"check": w_check, "bit": w_bit, "source": "phase shader-clock shares, profiles/r06_variants.txt"},
+           "dynamic_per_launch": dict(sorted(mix.items(), key=lambda kv: -kv[1])),
+           "note": "relative mix only (sums to the weights' total): pricing takes composition, not counts"}
+    with open(out_path, "w") as f:
+        json.dump(rec, f, indent=1)
+    return rec
+
+
 def main(argv):
+    if argv[1] == "variant":
+        rec = census_variant(argv[2], argv[3], float(argv[4]), float(argv[5]), argv[6])
+        costs = load_costs()
+        for k, v in sorted(class_prices(rec["dynamic_per_launch"], costs).items(), key=lambda kv: -kv[1]["count"]):
+            print(f"  {k:10s} {v['count']:8.3f}  {v['cycles'] or 0:5.2f} cyc  measured {v['measured_share']:.3f}")
+        return
     if argv[1] == "census":
         rec = census(argv[2], argv[3], argv[4])
         tot = sum(rec["dynamic_per_launch"].values())
