@@ -190,6 +190,14 @@ template <> struct BufIo<double> {
     static __device__ __forceinline__ double ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
     }
+    // a lane offset plus a wave-uniform one (soffset: scalar arithmetic only)
+    static __device__ __forceinline__ double ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+    }
+    static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double v) {
+        using V = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V, v), r, (int)voff, (int)soff, 0);
+    }
     static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
         using V = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V, v), r, (int)off, 0, 0);
@@ -917,13 +925,20 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
 #ifndef QKD_R1_SPLIT
 #define QKD_R1_SPLIT 1
 #endif
+    // a fixed global row's slot as the lane's byte offset, loop-invariant,
+    // plus the wave-uniform rest in soffset: no per-access vector address
+    // arithmetic (iw = the wave's first bit of the round)
+    const uint32_t vlane = (uint32_t)lane * 8u;
+    auto gsoff = [&](int k, uint32_t iw) -> uint32_t {
+        return ms.gofs((uint32_t)k * n_pad + iw);
+    };
     auto ld_k = [&](auto fx, int k, uint32_t iw, uint32_t i) -> double {
         const uint32_t x = (uint32_t)k * n_pad + i;
         if constexpr (decltype(fx)::value >= 1) {
             if (k == 0) return ms.l[x];
-            if (k == 2) return BufIo<double>::ld(ms.gw, ms.gofs(x));
+            if (k == 2) return BufIo<double>::ld(ms.gw, vlane, gsoff(k, iw));
             if constexpr (decltype(fx)::value == 2) return ms.l[x];
-            if constexpr (decltype(fx)::value == 3) return BufIo<double>::ld(ms.gw, ms.gofs(x));
+            if constexpr (decltype(fx)::value == 3) return BufIo<double>::ld(ms.gw, vlane, gsoff(k, iw));
         }
         return ms.ld_row((uint32_t)k * n_pad + iw, x);
     };
@@ -931,13 +946,20 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
         const uint32_t x = (uint32_t)k * n_pad + i;
         if constexpr (decltype(fx)::value >= 1) {
             if (k == 0) { ms.l[x] = v; return; }
-            if (k == 2) { BufIo<double>::st(ms.gw, ms.gofs(x), v); return; }
+            if (k == 2) { BufIo<double>::st(ms.gw, vlane, gsoff(k, iw), v); return; }
             if constexpr (decltype(fx)::value == 2) { ms.l[x] = v; return; }
-            if constexpr (decltype(fx)::value == 3) { BufIo<double>::st(ms.gw, ms.gofs(x), v); return; }
+            if constexpr (decltype(fx)::value == 3) { BufIo<double>::st(ms.gw, vlane, gsoff(k, iw), v); return; }
         }
         ms.st_row((uint32_t)k * n_pad + iw, x, v);
     };
     const uint32_t lsign = (uint32_t)qkdm::hi32(a.log_p) >> 31;
+    // the LLR interval's bounds as a VGPR pair made once (as kernel arguments
+    // they spilled to VGPR lanes and every round read them back with
+    // v_readlane and moved them into VGPRs for its select: -15 % of the bit
+    // rounds' VALU with the soffset slots above, profiles/r06_ab.txt)
+    qkds::f2 lpv;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lpv.x) : "s"(a.lp_dn));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lpv.y) : "s"(a.lp_up));
     // one batch of kIvChunk rounds: its loads, then its rounds
     typedef double VB[kIvChunk][kDvUnroll];
     auto batch_load = [&](auto fx, int r0, VB& v, uint64_t (&bc)[kIvChunk], uint32_t (&pat)[kIvChunk]) {
@@ -1015,7 +1037,7 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             } else {
                 f2 L;
                 if constexpr (MODE == kModeLlr) L = qkds::iv_of(ok ? a.llr[(size_t)f * c.n + c.perm[i]] : 0.0);
-                else L = bob ? f2{-a.lp_up, -a.lp_dn} : f2{a.lp_dn, a.lp_up};
+                else L = bob ? f2{-lpv.y, -lpv.x} : lpv;
                 f2 cs[kDvUnroll];
                 f2 T = L;
                 // max(|lo|, |hi|) of an interval lo <= hi is max(hi, -lo) (med3
@@ -1034,7 +1056,10 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
                 }
                 // binary32 roundings (the sum here and the subtraction below)
                 // and the reference's binary64 ones, relative to the magnitudes
-                const float mg = mag * ((float)(kDvUnroll + 2) * qkds::kSumRel) + 1.0e-30f;
+                // (one fma: kSumRel carries twice the rounding it covers, so the
+                // single rounding of the fused form is covered as the two of
+                // the product-then-sum were)
+                const float mg = __builtin_fmaf(mag, (float)(kDvUnroll + 2) * qkds::kSumRel, 1.0e-30f);
                 T = T + f2{-mg, mg};
                 // z = total <= 0 (:259), certain only if the interval says so
                 const bool z1 = T.y <= 0.0f;
@@ -1061,15 +1086,24 @@ __device__ __forceinline__ void spec_bit_phase(const DeviceCode& c, const Decode
             const bool flip =
                 kRunSyn ? (ok && z != (((zw[(r * kDecodeBlock >> 6) + wave] >> lane) & 1ull) != 0)) : z;
             if (lane == 0 && wave_in) zw[(r * kDecodeBlock >> 6) + wave] = zb;
+            // (each check's word and bit formed inside the branch, behind an
+            // empty asm: hoisted above it, they cost every round their VALU
+            // although many rounds of a wave flip no decision; -0.7 %)
             if (flip) {
 #pragma unroll
-                for (int k = 0; k < kDvUnroll; ++k)
-                    if (DV3 || k < deg) atomicXor(&xsyn[jc[k] >> 5], 1u << (jc[k] & 31));
+                for (int k = 0; k < kDvUnroll; ++k) {
+                    int32_t j = jc[k];
+                    asm volatile("" : "+v"(j));
+                    if (DV3 || k < deg) atomicXor(&xsyn[j >> 5], 1u << (j & 31));
+                }
             }
             if (unc) {
 #pragma unroll
-                for (int k = 0; k < kDvUnroll; ++k)
-                    if (DV3 || k < deg) atomicOr(&xunc[jc[k] >> 5], 1u << (jc[k] & 31));
+                for (int k = 0; k < kDvUnroll; ++k) {
+                    int32_t j = jc[k];
+                    asm volatile("" : "+v"(j));
+                    if (DV3 || k < deg) atomicOr(&xunc[j >> 5], 1u << (j & 31));
+                }
             }
             if (!keep) continue;
             if (DV3 && full) {
