@@ -227,12 +227,14 @@ def test_interleaved_global_targets_equal_split(Q, monkeypatch, q, qkd_opt):
     assert torch.equal(x.syndromes_match, y.syndromes_match) and torch.equal(x.keys_match, y.keys_match)
 
 
-@pytest.fixture(scope="module", params=[70002, 80002])
+@pytest.fixture(scope="module", params=[70002, 80002, 131070])
 def long_codes(request, Q, oracle_mod, tmp_path_factory):
     """Codes past kMaxBitsSplit (65,536 bits): N = 70,002 (M = 35,001, the
-    interleaved decoder's target syndrome words in global memory) and 80,002
-    (M = 40,001: its uncertainty words there too, decode_ilv_kernel<..., UG>);
-    N mod 64 != 0 (a ragged last key word)."""
+    interleaved decoder's target syndrome words in global memory), 80,002
+    (M = 40,001: its uncertainty words there too, decode_ilv_kernel<..., UG>)
+    and 131,070 (M = 65,535: the largest the long-code path takes,
+    kMaxBitsSplitLong / kMaxChecksSplit); N mod 64 != 0 (a ragged last key
+    word)."""
     n = request.param
     m, cp, ci = regular_code(n, seed=5)
     H = Q.HMatrix.from_check_lists(n, cp, ci)
