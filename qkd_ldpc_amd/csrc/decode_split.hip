@@ -1365,9 +1365,6 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
             xunc[w] = 0;
         }
         __syncthreads();
-#ifdef QKD_PRO_MARKS
-        pc.mark(5);      // (diagnostic: the loop top's clear and barrier as phase 5)
-#endif
         const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl[1]);   // (uniform to the compiler)
         if (f >= a.n_frames) break;
         if (tid == 0) next_f = claim();
@@ -1396,9 +1393,6 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                 qsyn[q] = sy[m_words + q];
             }
             __syncthreads();
-#ifdef QKD_PRO_MARKS
-            pc.mark(6);  // (diagnostic: the frame's loads and their barrier as phase 6)
-#endif
         }
         // Bob's bits of this thread's bit-phase rounds (round r: internal bit
         // i = tid + r * kDecodeBlock; N <= 64 * kDecodeBlock, kMaxBitsSplit).
@@ -1541,11 +1535,7 @@ __global__ QKD_SPLIT_BOUNDS void decode_split_kernel(DecodeArgs a) {
                                                                    wave, lane);
                 __syncthreads();
             }
-#ifdef QKD_PRO_MARKS
-            pc.mark(1);
-#else
             pc.mark((FOLDS && it < 2 && fold1) ? 5 + (int)it : 1);
-#endif
             // the b2c of this bit phase are read only by a next iteration
             const bool keep = it + 1 < a.max_it;
             // bit phase: total_i = LLR_i + sum_k c2b[k][i], ascending checks (:256-267),
