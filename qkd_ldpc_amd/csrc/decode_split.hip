@@ -1962,9 +1962,26 @@ __global__ void zout_unpack_kernel(const uint64_t* zout, const int32_t* inv, uin
 constexpr int kSlicedFrames = 16;
 constexpr int kSlicedBlock = 1024;
 constexpr int kSlicedPre = 8;        // key-word pairs a wave loads ahead
-// lane `at` (wave-uniform) of x takes the wave-uniform value m
-__device__ __forceinline__ uint64_t put_lane(uint64_t x, uint32_t at, uint64_t m) {
-    return (threadIdx.x & 63u) == at ? m : x;
+// A bit transpose within each 32-lane half of the wave: afterwards lane 32 h +
+// c holds in bit r what lane 32 h + r held in bit c. Five butterfly stages
+// (s = 16 ... 1): lane l takes its partner l ^ s's value through ds_swizzle,
+// rotates it by s toward the bit block it trades (one v_alignbit_b32) and
+// keeps its own other block (one v_bfi_b32) -- 2 VALU and a swizzle per stage
+// where a ballot per bit and a lane select per bit took ~15 VALU per bit.
+template <int S, uint32_t MASK>
+__device__ __forceinline__ uint32_t transpose_stage(uint32_t x, uint32_t lane) {
+    const uint32_t y = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (S << 10));   // lane ^ S
+    const bool hi = (lane & (uint32_t)S) != 0;
+    const uint32_t ys = __builtin_amdgcn_alignbit(y, y, hi ? (uint32_t)S : 32u - (uint32_t)S);
+    const uint32_t k = hi ? ~MASK : MASK;
+    return (x & k) | (ys & ~k);
+}
+__device__ __forceinline__ uint32_t wave_transpose32(uint32_t x, uint32_t lane) {
+    x = transpose_stage<16, 0x0000FFFFu>(x, lane);
+    x = transpose_stage<8, 0x00FF00FFu>(x, lane);
+    x = transpose_stage<4, 0x0F0F0F0Fu>(x, lane);
+    x = transpose_stage<2, 0x33333333u>(x, lane);
+    return transpose_stage<1, 0x55555555u>(x, lane);
 }
 // BYTES (qkd_qkd_ldpc_batch's byte keys, N % 8 == 0, rows 8-byte aligned): the
 // slices come straight from the caller's 0/1 bytes, and alice_w / bob_w are
@@ -2002,19 +2019,16 @@ __global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCo
         return (bob_lane ? bob_w : alice_w)[(size_t)(f0 + fr) * words + w];
     };
     auto slice_pair = [&](uint32_t p, uint64_t v) {
-        // (four independent select chains: each lane takes exactly one value)
-        uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-        const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
-#pragma unroll
-        for (uint32_t b = 0; b < 32; b += 2) {
-            m0 = put_lane(m0, b, __ballot((vlo >> b) & 1u));
-            m1 = put_lane(m1, b + 1, __ballot((vlo >> (b + 1)) & 1u));
-            m2 = put_lane(m2, 32 + b, __ballot((vhi >> b) & 1u));
-            m3 = put_lane(m3, 33 + b, __ballot((vhi >> (b + 1)) & 1u));
+        // the lanes of half h hold word 2p + h of the 16 frames' keys (lane
+        // 16 key + frame): transposed, lane 32 h + c holds the slice of that
+        // word's bit c (low 32 bits) or bit 32 + c (high)
+        const uint32_t tlo = wave_transpose32((uint32_t)v, lane);
+        const uint32_t thi = wave_transpose32((uint32_t)(v >> 32), lane);
+        const uint32_t w = 2 * p + half, b = lane & 31u;
+        if (w < words) {
+            T[(size_t)w * 64 + b] = tlo;
+            T[(size_t)w * 64 + 32 + b] = thi;
         }
-        const uint64_t mine = m0 | m1 | m2 | m3;
-        T[(size_t)(2 * p) * 64 + lane] = (uint32_t)mine;
-        if (2 * p + 1 < words) T[(size_t)(2 * p + 1) * 64 + lane] = (uint32_t)(mine >> 32);
     };
     if constexpr (BYTES) {
         const uint32_t n = (uint32_t)c.n;
@@ -2083,33 +2097,38 @@ __global__ __launch_bounds__(kSlicedBlock) void frame_syn_sliced_kernel(DeviceCo
             }
         }
         const uint32_t Q = P ^ (P >> 16) ^ ((lsign & deg) ? 0xffffu : 0u);   // low 16: q bits
-        uint64_t sk = 0, qk = 0;
-        for (uint32_t f = 0; f < nf; ++f) {
-            sk = put_lane(sk, f, __ballot((P >> f) & 1u));
-            qk = put_lane(qk, f, __ballot((Q >> f) & 1u));
-        }
-        if (lane < nf) {
-            uint32_t* o = synw + (size_t)(f0 + lane) * 2 * m_words;
-            o[j0 >> 5] = (uint32_t)sk;
-            o[(j0 >> 5) + 1] = (uint32_t)(sk >> 32);
-            o[m_words + (j0 >> 5)] = (uint32_t)qk;
-            o[m_words + (j0 >> 5) + 1] = (uint32_t)(qk >> 32);
+        // transposed, lane f < 16 holds frame f's target bits of the 64 checks
+        // (its own value the low word, lane 32 + f's the high) and lane 16 + f
+        // its q bits; both go out as one 8-byte store (m_words and j0 / 32 even)
+        const uint32_t tr = wave_transpose32((P & 0xffffu) | (Q << 16), lane);
+        const uint32_t up = (uint32_t)__shfl_xor((int)tr, 32);
+        const uint32_t g = lane & 15u;
+        if (lane < 32 && g < nf) {
+            uint32_t* o = synw + (size_t)(f0 + g) * 2 * m_words + (lane < 16 ? 0 : m_words) + (j0 >> 5);
+            *reinterpret_cast<uint2*>(o) = make_uint2(tr, up);
         }
     }
     // 3. the keys in the internal order (DeviceCode::perm), in place: word w's
-    //    lane l reads the slice of original bit perm[64 w + l]; per frame a
-    //    ballot per key, lane f keeping Alice's word of frame f, lane 32 + f Bob's
-    for (uint32_t w = wave; w < words; w += NW) {
+    //    lane l reads the slice of original bit perm[64 w + l] (the perm entry
+    //    of the wave's next word loaded a word ahead, through a clamped index:
+    //    no branch around the load); transposed, lane f < 16 holds Alice's word
+    //    of frame f (high half from lane 32 + f), lane 16 + f Bob's
+    const uint32_t cn = (uint32_t)c.n;
+    auto perm_at = [&](uint32_t w) -> uint32_t {
         const uint32_t q = w * 64 + lane;
-        const uint32_t S = q < (uint32_t)c.n ? T[c.perm[q]] : 0u;
-        uint64_t ma = 0, mb = 0;
-        for (uint32_t f = 0; f < nf; ++f) {
-            ma = put_lane(ma, f, __ballot((S >> f) & 1u));
-            mb = put_lane(mb, 32 + f, __ballot((S >> (16 + f)) & 1u));
-        }
-        const uint64_t mine = ma | mb;
-        const uint32_t g = lane & 31u;
-        if (g < nf) (lane < 32 ? alice_w : bob_w)[(size_t)(f0 + g) * words + w] = mine;
+        return c.perm[q < cn ? q : 0u];
+    };
+    uint32_t pq = perm_at(wave < (uint32_t)words ? wave : 0u);
+    for (uint32_t w = wave; w < words; w += NW) {
+        const uint32_t wn = w + NW;
+        const uint32_t pn = perm_at(wn < (uint32_t)words ? wn : w);
+        const uint32_t S = w * 64 + lane < cn ? T[pq] : 0u;
+        const uint32_t tr = wave_transpose32(S, lane);
+        const uint32_t up = (uint32_t)__shfl_xor((int)tr, 32);
+        const uint32_t g = lane & 15u;
+        if (lane < 32 && g < nf)
+            (lane < 16 ? alice_w : bob_w)[(size_t)(f0 + g) * words + w] = ((uint64_t)up << 32) | tr;
+        pq = pn;
     }
 }
 
