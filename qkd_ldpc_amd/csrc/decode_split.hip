@@ -169,6 +169,9 @@ __device__ __forceinline__ uint2 plan_word(__amdgpu_buffer_rsrc_t plan, int t, i
     return __builtin_bit_cast(uint2, v);
 }
 
+// a wave mask folded to 32 bits, nonzero iff the mask is (scalar ors)
+__device__ __forceinline__ uint32_t fold64(uint64_t m) { return (uint32_t)m | (uint32_t)(m >> 32); }
+
 // [lo, hi] negated: [-hi, -lo] when neg. Written per element, so each half is
 // one v_cndmask_b32 with a negated source (the vector form costs a packed
 // negation and a swap besides).
@@ -646,7 +649,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
     if (t >= n_tasks) return;
     const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
     // lanes that could not certify (wave masks: scalar ors, no per-lane flag)
-    uint64_t bad = 0;
+    uint32_t bad = 0;
     // the row's DC entries past lane 63 are read (times 0) by segments ending
     // there: keep them finite (the prologue stages key words in this region)
     if (lane < DC) row[64 + lane] = 0.0;
@@ -662,7 +665,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         // what it does to the other lanes' sums never stands; the dummy
         // column's entry is finite. Two ballots of plain compares: a ballot of
         // their conjunction materialises it as 0 / 1 and compares it back)
-        bad |= __ballot(!ok) & __ballot(pw_slot(w) != dummy);
+        bad |= fold64(__ballot(!ok) & __ballot(pw_slot(w) != dummy));
         return neg_iv_if(neg, bv);
     };
     uint2 wt = plan_word(prs, t, lane);
@@ -694,7 +697,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
         f2 ext = sum + f2{-mg, mg};
         ext.x = ext.x > 0.0f ? ext.x : 0.0f;
-        bad |= __ballot(!(ext.y < qkds::kPsiSumMax));      // the reference's product would underflow
+        bad |= fold64(__ballot(!(ext.y < qkds::kPsiSumMax)));      // the reference's product would underflow
         f2 m = qkds::phi_bounds_out(ext.x, ext.y);
         // threshold_matrix (:246-249) on the magnitude
         // (m >= 0, not NaN: med3 with 0 is the min, without the per-edge
@@ -707,7 +710,7 @@ __device__ __forceinline__ void spec_check_phase_psi(const uint2* __restrict__ p
         sgn_t = __ballot(neg_n);
         neg_t = neg_n;
         sb_t = sb_n;
-        t += NW;
+        t = __builtin_amdgcn_readfirstlane(t + NW);
         return t < n_tasks;
     };
     Raw xa = ms.ld_raw(slot(wn)), xb;
@@ -741,7 +744,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
     if (t >= n_tasks) return;
     const __amdgpu_buffer_rsrc_t prs = plan_rsrc(plan);
     // lanes that could not certify (wave masks: scalar ors, no per-lane flag)
-    uint64_t bad = 0;
+    uint32_t bad = 0;
     if (lane < DC) row[64 + lane] = 0.0;
     auto slot = [&](uint2 p) -> uint32_t { return pw_slot(p); };
     // |b2c| of an edge, its sign and whether the interval certifies it
@@ -754,7 +757,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         // |.|lo > 1e-30, of which the second alone decides: |.|lo is -hi
         // when neg, lo otherwise; NaN fails either way)
         const bool ok = ab.x > 1.0e-30f;
-        bad |= __ballot(!ok) & __ballot(pw_slot(w) != dummy);
+        bad |= fold64(__ballot(!ok) & __ballot(pw_slot(w) != dummy));
         return ok;
     };
     // (the plan has kPlanPadTasks idle tasks past n_tasks: loads ahead need no test)
@@ -795,7 +798,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         const float mg = __builtin_fmaf(sum.y, nr * qkds::kSumRel, qkds::kRefSumAbs);
         f2 ext = sum + f2{-mg, mg};
         ext.x = ext.x > 0.0f ? ext.x : 0.0f;
-        bad |= __ballot(!(ext.y < qkds::kPsiSumMax));
+        bad |= fold64(__ballot(!(ext.y < qkds::kPsiSumMax)));
         f2 ph_n, m;
         qkds::phi_pair(ab_n.x, ab_n.y, ext.x, ext.y, ph_n, m);
         // this task's c2b: threshold_matrix (:246-249) on the magnitude, the sign
@@ -811,7 +814,7 @@ __device__ __forceinline__ void spec_check_phase_paired(const uint2* __restrict_
         sgn_t = __ballot(neg_n);
         neg_t = neg_n;
         sb_t = sb_n;
-        t += NW;
+        t = __builtin_amdgcn_readfirstlane(t + NW);
         return t < n_tasks;
     };
     Raw xa = ms.ld_raw(slot(wn)), xb;
