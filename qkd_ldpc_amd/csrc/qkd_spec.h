@@ -230,7 +230,12 @@ __device__ __forceinline__ void phi_pair(float a, float b, float s_lo, float s_h
     const f2 hi = __builtin_elementwise_fma(v, f2(kPhiRel), v) + f2(1.0e-37f);
     // (the interval widths elementwise: two scalar subtractions straight into
     // the pair, where a packed one needs both operand pairs assembled first)
-    const f2 dd = f2{b - a1, s_hi - P};
+    // (each an empty asm's operand: left alone, the SLP vectorizer packs the
+    // two into a v_pk_add_f32 whose operand pairs take two moves to build)
+    float d0 = b - a1, d1 = s_hi - P;
+    asm("" : "+v"(d0));
+    asm("" : "+v"(d1));
+    const f2 dd = f2{d0, d1};
     const f2 tn = __builtin_elementwise_fma(
         -slope * f2{(1.0f + 2.0f * kPhiRel) * kInvLn2, (1.0f + 2.0f * kPhiRel) * kLn2}, dd,
         v * f2(1.0f - kPhiRel));
